@@ -1,0 +1,468 @@
+"""MI355X-native ray-tracing hot path of pmichels19/AdvancedGraphicsRayTracer.
+
+Python face of librtamd.so (C-ABI in include/rt_amd.h).  The classes mirror the
+reference's C++ surface for this path:
+
+    Scene.IntersectBVH / Scene.IsOccluded   <- Scene::IntersectBVH / IsOccluded (template/scene.h:285, 452)
+    Renderer.Tick                            <- Renderer::Tick (renderer.cpp:200-309)
+    Camera                                   <- Camera (camera.h:28-52)
+
+Everything computes on the GPU through librtamd.so; there is no CPU fallback.  A
+missing library or device raises RTError.  Device buffers are torch tensors (torch is
+plumbing here: memory, streams, torch.distributed).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "librtamd.so")
+DATA_DIR = os.path.join(PKG_DIR, "data")
+HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "rt_amd.h")
+
+RT_OK, RT_ERR_INVALID, RT_ERR_NO_DEVICE, RT_ERR_HIP, RT_ERR_IO, RT_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5
+SPHERE, PLANE, TRIANGLE = 0, 1, 4
+DIFFUSE, MIRROR, DIELECTRIC, CHECKERBOARD, LIGHT = 0, 1, 2, 3, 4
+MODE_PATH = 0
+RECIPES = ("teapotF", "teapot", "mig16", "cfg3", "cfg5")
+
+
+class RTError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class Prim(C.Structure):
+    _fields_ = [("type", C.c_int32), ("material", C.c_int32), ("v", C.c_float * 9)]
+
+
+class Material(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("color", C.c_float * 3), ("color2", C.c_float * 3), ("ior", C.c_float),
+                ("diffuse", C.c_float)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("prims", C.POINTER(Prim)), ("num_prims", C.c_uint32),
+                ("materials", C.POINTER(Material)), ("num_materials", C.c_uint32),
+                ("sky_pixels", C.POINTER(C.c_uint32)), ("sky_width", C.c_uint32), ("sky_height", C.c_uint32),
+                ("bvh_nodes", C.c_void_p), ("bvh_num_nodes", C.c_uint32), ("bvh_indices", C.POINTER(C.c_uint32)),
+                ("device", C.c_int32)]
+
+
+class SceneInfo(C.Structure):
+    _fields_ = [("num_prims", C.c_uint32), ("nodes_used", C.c_uint32), ("depth", C.c_uint32), ("max_leaf", C.c_uint32)]
+
+
+class Camera(C.Structure):
+    """Camera state (camera.h:93-100)."""
+    _fields_ = [("pos", C.c_float * 3), ("top_left", C.c_float * 3), ("top_right", C.c_float * 3),
+                ("bottom_left", C.c_float * 3), ("lens_radius", C.c_float)]
+
+    @classmethod
+    def default(cls, width, height):
+        cam = cls()
+        _check(lib().rt_camera_default(width, height, C.byref(cam)))
+        return cam
+
+
+class FrameParams(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("width", "height", "spp", "depth", "frame", "mode", "reset")]
+
+
+class Counters(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("primary", "shadow", "bounce", "frames")]
+
+
+RAY_DTYPE = np.dtype([("o", "<f4", 3), ("d", "<f4", 3), ("tmax", "<f4")])
+HIT_DTYPE = np.dtype([("t", "<f4"), ("obj", "<i4"), ("u", "<f4"), ("v", "<f4")])
+
+_lib = None
+
+
+def lib():
+    """Load librtamd.so.  Raises RTError when the native library is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RTError(RT_ERR_NO_DEVICE, f"{LIB_PATH} not built (run __graft_entry__.build()); no CPU fallback exists")
+    L = C.CDLL(LIB_PATH)
+    vp, u32, i32, f = C.c_void_p, C.c_uint32, C.c_int32, C.c_float
+    fp = C.POINTER(C.c_float)
+    sigs = {
+        "rt_abi_version": ([], C.c_int),
+        "rt_last_error": ([], C.c_char_p),
+        "rt_device_count": ([C.POINTER(C.c_int)], C.c_int),
+        "rt_free": ([vp], None),
+        "rt_obj_load": ([C.c_char_p, C.POINTER(fp), C.POINTER(u32), C.POINTER(C.POINTER(i32)), C.POINTER(u32)], C.c_int),
+        "rt_mesh_load": ([C.c_char_p, C.POINTER(fp), C.POINTER(u32), C.POINTER(C.POINTER(i32)), C.POINTER(u32)], C.c_int),
+        "rt_mesh_save": ([C.c_char_p, fp, u32, C.POINTER(i32), u32], C.c_int),
+        "rt_mat4_translate": ([f, f, f, fp], C.c_int),
+        "rt_mat4_scale": ([f, fp], C.c_int),
+        "rt_mat4_rotate": ([C.c_int, f, fp], C.c_int),
+        "rt_mat4_mul": ([fp, fp, fp], C.c_int),
+        "rt_mesh_to_prims": ([fp, u32, C.POINTER(i32), u32, fp, i32, C.POINTER(Prim)], C.c_int),
+        "rt_recipe_describe": ([C.c_char_p, C.c_char_p, C.POINTER(Prim), C.POINTER(u32), C.POINTER(Material),
+                                C.POINTER(u32)], C.c_int),
+        "rt_bvh_build_host": ([C.POINTER(Prim), u32, vp, C.POINTER(u32), C.POINTER(SceneInfo)], C.c_int),
+        "rt_scene_create": ([C.POINTER(SceneDesc), C.POINTER(vp)], C.c_int),
+        "rt_scene_create_recipe": ([C.c_char_p, C.c_char_p, i32, C.POINTER(vp)], C.c_int),
+        "rt_scene_destroy": ([vp], C.c_int),
+        "rt_scene_get_info": ([vp, C.POINTER(SceneInfo)], C.c_int),
+        "rt_scene_copy_bvh": ([vp, vp, C.POINTER(u32)], C.c_int),
+        "rt_intersect": ([vp, vp, vp, u32, vp], C.c_int),
+        "rt_occluded": ([vp, vp, vp, u32, vp], C.c_int),
+        "rt_intersect_host": ([vp, vp, vp, u32], C.c_int),
+        "rt_occluded_host": ([vp, vp, vp, u32], C.c_int),
+        "rt_camera_default": ([u32, u32, C.POINTER(Camera)], C.c_int),
+        "rt_renderer_create": ([vp, u32, u32, C.POINTER(vp)], C.c_int),
+        "rt_renderer_destroy": ([vp], C.c_int),
+        "rt_render_frame": ([vp, C.POINTER(Camera), C.POINTER(FrameParams), vp, vp], C.c_int),
+        "rt_render_frame_host": ([vp, C.POINTER(Camera), C.POINTER(FrameParams), vp], C.c_int),
+        "rt_shard_capacity": ([u32, u32, u32, C.POINTER(u32)], C.c_int),
+        "rt_render_shard": ([vp, C.POINTER(Camera), C.POINTER(FrameParams), u32, u32, vp, vp], C.c_int),
+        "rt_assemble_shards": ([vp, vp, u32, vp, vp], C.c_int),
+        "rt_renderer_counters": ([vp, C.POINTER(Counters)], C.c_int),
+        "rt_renderer_read_accumulator": ([vp, fp], C.c_int),
+        "rt_renderer_stream": ([vp, C.POINTER(vp)], C.c_int),
+        "rt_synchronize": ([vp], C.c_int),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    if L.rt_abi_version() != 1:
+        raise RTError(RT_ERR_INVALID, "librtamd.so ABI mismatch")
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != RT_OK:
+        raise RTError(rc, lib().rt_last_error().decode(errors="replace"))
+    return rc
+
+
+def device_count():
+    n = C.c_int(0)
+    rc = lib().rt_device_count(C.byref(n))
+    return n.value if rc == RT_OK else 0
+
+
+def _fptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+# ---------------------------------------------------------------- host-side scene preparation
+def load_obj(path):
+    """tinyobj-compatible OBJ read (Scene::LoadModel's input): (verts[nv,3] f32, faces[nt,3] i32)."""
+    return _take_mesh(lib().rt_obj_load, path)
+
+
+def load_mesh(path):
+    """RTMESH1 container read."""
+    return _take_mesh(lib().rt_mesh_load, path)
+
+
+def _take_mesh(fn, path):
+    L = lib()
+    vp, fp = C.POINTER(C.c_float)(), C.POINTER(C.c_int32)()
+    nv, nt = C.c_uint32(), C.c_uint32()
+    _check(fn(os.fsencode(path), C.byref(vp), C.byref(nv), C.byref(fp), C.byref(nt)))
+    try:
+        V = np.ctypeslib.as_array(vp, shape=(nv.value, 3)).copy() if nv.value else np.zeros((0, 3), np.float32)
+        F = np.ctypeslib.as_array(fp, shape=(nt.value, 3)).copy() if nt.value else np.zeros((0, 3), np.int32)
+    finally:
+        L.rt_free(C.cast(vp, C.c_void_p))
+        L.rt_free(C.cast(fp, C.c_void_p))
+    return V, F
+
+
+def save_mesh(path, verts, faces):
+    V = np.ascontiguousarray(verts, np.float32)
+    F = np.ascontiguousarray(faces, np.int32)
+    _check(lib().rt_mesh_save(os.fsencode(path), _fptr(V), len(V), F.ctypes.data_as(C.POINTER(C.c_int32)), len(F)))
+
+
+def mat4_translate(x, y, z):
+    m = np.zeros(16, np.float32)
+    _check(lib().rt_mat4_translate(x, y, z, _fptr(m)))
+    return m
+
+
+def mat4_scale(s):
+    m = np.zeros(16, np.float32)
+    _check(lib().rt_mat4_scale(s, _fptr(m)))
+    return m
+
+
+def mat4_rotate(axis, angle):
+    m = np.zeros(16, np.float32)
+    _check(lib().rt_mat4_rotate(axis, angle, _fptr(m)))
+    return m
+
+
+def mat4_mul(*ms):
+    acc = np.ascontiguousarray(ms[0], np.float32).copy()
+    for m in ms[1:]:
+        m = np.ascontiguousarray(m, np.float32)
+        out = np.zeros(16, np.float32)
+        _check(lib().rt_mat4_mul(_fptr(acc), _fptr(m), _fptr(out)))
+        acc = out
+    return acc
+
+
+def mesh_to_prims(verts, faces, M, material):
+    """Scene::LoadModel's face loop: one triangle per face, vertices TransformPosition'ed by M."""
+    V = np.ascontiguousarray(verts, np.float32)
+    F = np.ascontiguousarray(faces, np.int32)
+    Mm = np.ascontiguousarray(M, np.float32)
+    out = (Prim * len(F))()
+    _check(lib().rt_mesh_to_prims(_fptr(V), len(V), F.ctypes.data_as(C.POINTER(C.c_int32)), len(F), _fptr(Mm),
+                                  material, out))
+    return list(out)
+
+
+def recipe_describe(name, mesh_dir=DATA_DIR):
+    """The SURVEY.md 8(d) scene as (prims, materials) lists, without touching a device."""
+    L = lib()
+    n, m = C.c_uint32(), C.c_uint32()
+    _check(L.rt_recipe_describe(name.encode(), os.fsencode(mesh_dir), None, C.byref(n), None, C.byref(m)))
+    pa, ma = (Prim * n.value)(), (Material * m.value)()
+    _check(L.rt_recipe_describe(name.encode(), os.fsencode(mesh_dir), pa, C.byref(n), ma, C.byref(m)))
+    return list(pa), list(ma)
+
+
+def build_bvh_host(prims):
+    """Plain binned-SAH BVH on the host (template/scene.h:845-976): (nodes[n,32] u8, indices, info)."""
+    arr = (Prim * len(prims))(*prims)
+    nodes = np.zeros((2 * len(prims) + 2, 32), np.uint8)
+    idx = np.zeros(len(prims), np.uint32)
+    info = SceneInfo()
+    _check(lib().rt_bvh_build_host(arr, len(prims), nodes.ctypes.data_as(C.c_void_p),
+                                   idx.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(info)))
+    return nodes[:info.nodes_used], idx, _info_dict(info)
+
+
+def _info_dict(info):
+    return {"num_prims": info.num_prims, "nodes_used": info.nodes_used, "depth": info.depth, "max_leaf": info.max_leaf}
+
+
+def sphere(center, radius, material):
+    p = Prim(SPHERE, material)
+    p.v[0], p.v[1], p.v[2], p.v[3] = center[0], center[1], center[2], radius
+    return p
+
+
+def plane(normal, distance, material):
+    p = Prim(PLANE, material)
+    p.v[0], p.v[1], p.v[2], p.v[3] = normal[0], normal[1], normal[2], distance
+    return p
+
+
+def triangle(a, b, c, material):
+    p = Prim(TRIANGLE, material)
+    for k, q in enumerate((a, b, c)):
+        p.v[3 * k], p.v[3 * k + 1], p.v[3 * k + 2] = q
+    return p
+
+
+def material(kind, color=(0, 0, 0), color2=(0, 0, 0), ior=0.0, diffuse=-1.0):
+    m = Material(kind)
+    m.color[:] = color
+    m.color2[:] = color2
+    m.ior = ior
+    m.diffuse = diffuse
+    return m
+
+
+# ---------------------------------------------------------------- device objects
+def _torch():
+    import torch
+    return torch
+
+
+def _as_device_rays(rays, device):
+    torch = _torch()
+    if isinstance(rays, torch.Tensor):
+        t = rays
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(rays, np.float32).reshape(-1, 7))
+    return t.to(device=f"cuda:{device}", dtype=torch.float32).contiguous().reshape(-1, 7)
+
+
+class Scene:
+    """Scene (template/scene.h:37): primitives + materials + plain BVH, resident in HBM."""
+
+    def __init__(self, prims=None, materials=None, sky=None, bvh=None, device=0, _handle=None):
+        self.L = lib()
+        self.device = device
+        self.h = C.c_void_p()
+        if _handle is not None:
+            self.h = _handle
+            return
+        pa = (Prim * len(prims))(*prims)
+        ma = (Material * len(materials))(*materials)
+        d = SceneDesc()
+        d.prims, d.num_prims = pa, len(prims)
+        d.materials, d.num_materials = ma, len(materials)
+        d.device = device
+        keep = []
+        if sky is not None:
+            sky = np.ascontiguousarray(sky, np.uint32)
+            d.sky_pixels = sky.ctypes.data_as(C.POINTER(C.c_uint32))
+            d.sky_height, d.sky_width = sky.shape
+            keep.append(sky)
+        if bvh is not None:
+            nodes, idx = np.ascontiguousarray(bvh[0], np.uint8), np.ascontiguousarray(bvh[1], np.uint32)
+            d.bvh_nodes = nodes.ctypes.data_as(C.c_void_p)
+            d.bvh_num_nodes = len(nodes)
+            d.bvh_indices = idx.ctypes.data_as(C.POINTER(C.c_uint32))
+            keep += [nodes, idx]
+        _check(self.L.rt_scene_create(C.byref(d), C.byref(self.h)))
+
+    @classmethod
+    def recipe(cls, name, mesh_dir=DATA_DIR, device=0):
+        """One of the SURVEY.md 8(d) benchmark scenes ("teapotF", "teapot", "mig16", "cfg3", "cfg5")."""
+        h = C.c_void_p()
+        _check(lib().rt_scene_create_recipe(name.encode(), os.fsencode(mesh_dir), device, C.byref(h)))
+        return cls(device=device, _handle=h)
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            self.L.rt_scene_destroy(self.h)
+            self.h = C.c_void_p()
+
+    __del__ = close
+
+    @property
+    def info(self):
+        i = SceneInfo()
+        _check(self.L.rt_scene_get_info(self.h, C.byref(i)))
+        return _info_dict(i)
+
+    def bvh(self):
+        info = self.info
+        nodes = np.zeros((info["nodes_used"], 32), np.uint8)
+        idx = np.zeros(info["num_prims"], np.uint32)
+        _check(self.L.rt_scene_copy_bvh(self.h, nodes.ctypes.data_as(C.c_void_p),
+                                        idx.ctypes.data_as(C.POINTER(C.c_uint32))))
+        return nodes, idx
+
+    def IntersectBVH(self, rays, stream=None):
+        """Batched Scene::IntersectBVH.  rays: (n,7) [O, D, tmax] numpy or torch.
+        Returns (t f32, obj i32, u f32, v f32) torch tensors on the scene's device."""
+        torch = _torch()
+        r = _as_device_rays(rays, self.device)
+        n = r.shape[0]
+        hits = torch.empty((n, 4), dtype=torch.float32, device=r.device)
+        if n:
+            s = stream if stream is not None else torch.cuda.current_stream(r.device).cuda_stream
+            _check(self.L.rt_intersect(self.h, C.c_void_p(r.data_ptr()), C.c_void_p(hits.data_ptr()), n, C.c_void_p(s)))
+        return hits[:, 0], hits.view(torch.int32)[:, 1], hits[:, 2], hits[:, 3]
+
+    def IsOccluded(self, rays, stream=None):
+        """Batched Scene::IsOccluded: bool tensor."""
+        torch = _torch()
+        r = _as_device_rays(rays, self.device)
+        n = r.shape[0]
+        out = torch.empty(n, dtype=torch.uint8, device=r.device)
+        if n:
+            s = stream if stream is not None else torch.cuda.current_stream(r.device).cuda_stream
+            _check(self.L.rt_occluded(self.h, C.c_void_p(r.data_ptr()), C.c_void_p(out.data_ptr()), n, C.c_void_p(s)))
+        return out.bool()
+
+    def intersect_host(self, rays):
+        """Host-array variant (copies through the library's staging buffer)."""
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 7)
+        hits = np.zeros(len(rays), HIT_DTYPE)
+        _check(self.L.rt_intersect_host(self.h, rays.ctypes.data_as(C.c_void_p), hits.ctypes.data_as(C.c_void_p),
+                                        len(rays)))
+        return hits
+
+    def occluded_host(self, rays):
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 7)
+        out = np.zeros(len(rays), np.uint8)
+        _check(self.L.rt_occluded_host(self.h, rays.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p),
+                                       len(rays)))
+        return out.astype(bool)
+
+
+class Renderer:
+    """Renderer (renderer.h:5-160): owns the float4 accumulator; Tick = one frame."""
+
+    def __init__(self, scene, width, height):
+        self.L = lib()
+        self.scene = scene
+        self.width, self.height = width, height
+        self.camera = Camera.default(width, height)
+        self.h = C.c_void_p()
+        _check(self.L.rt_renderer_create(scene.h, width, height, C.byref(self.h)))
+        self.frame = 0
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            self.L.rt_renderer_destroy(self.h)
+            self.h = C.c_void_p()
+
+    __del__ = close
+
+    def params(self, spp=1, depth=10, frame=None, reset=False):
+        return FrameParams(self.width, self.height, spp, depth, self.frame if frame is None else frame, MODE_PATH,
+                           int(reset))
+
+    def Tick(self, out=None, spp=1, depth=10, frame=None, reset=False, stream=None):
+        """Renderer::Tick: trace, accumulate, pack RGB8 into out (torch uint32/int32 [H*W] on device)."""
+        torch = _torch()
+        if out is None:
+            out = torch.empty(self.width * self.height, dtype=torch.int32, device=f"cuda:{self.scene.device}")
+        p = self.params(spp, depth, frame, reset)
+        s = stream if stream is not None else torch.cuda.current_stream(out.device).cuda_stream
+        _check(self.L.rt_render_frame(self.h, C.byref(self.camera), C.byref(p), C.c_void_p(out.data_ptr()),
+                                      C.c_void_p(s)))
+        if frame is None:
+            self.frame += 1
+        return out
+
+    def tick_host(self, spp=1, depth=10, frame=None, reset=False):
+        """Renderer::Tick with the RGB8 frame returned in host memory (numpy uint32 [H*W])."""
+        out = np.zeros(self.width * self.height, np.uint32)
+        p = self.params(spp, depth, frame, reset)
+        _check(self.L.rt_render_frame_host(self.h, C.byref(self.camera), C.byref(p), out.ctypes.data_as(C.c_void_p)))
+        if frame is None:
+            self.frame += 1
+        return out
+
+    def shard_capacity(self, num_shards):
+        n = C.c_uint32()
+        _check(self.L.rt_shard_capacity(self.width, self.height, num_shards, C.byref(n)))
+        return n.value
+
+    def render_shard(self, out, shard, num_shards, spp=1, depth=10, frame=None, reset=False, stream=None):
+        torch = _torch()
+        p = self.params(spp, depth, frame, reset)
+        s = stream if stream is not None else torch.cuda.current_stream(out.device).cuda_stream
+        _check(self.L.rt_render_shard(self.h, C.byref(self.camera), C.byref(p), shard, num_shards,
+                                      C.c_void_p(out.data_ptr()), C.c_void_p(s)))
+        if frame is None:
+            self.frame += 1
+        return out
+
+    def assemble(self, gathered, num_shards, out, stream=None):
+        torch = _torch()
+        s = stream if stream is not None else torch.cuda.current_stream(out.device).cuda_stream
+        _check(self.L.rt_assemble_shards(self.h, C.c_void_p(gathered.data_ptr()), num_shards,
+                                         C.c_void_p(out.data_ptr()), C.c_void_p(s)))
+        return out
+
+    def counters(self):
+        c = Counters()
+        _check(self.L.rt_renderer_counters(self.h, C.byref(c)))
+        return {n: int(getattr(c, n)) for n, _ in Counters._fields_}
+
+    def accumulator(self):
+        acc = np.zeros((self.height * self.width, 4), np.float32)
+        _check(self.L.rt_renderer_read_accumulator(self.h, _fptr(acc)))
+        return acc

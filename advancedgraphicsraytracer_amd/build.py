@@ -1,0 +1,47 @@
+"""Build librtamd.so (host C++ + gfx950 HIP kernels) in-tree with hipcc.
+
+The library is the product: a C-ABI shared object whose entry points are declared in
+include/rt_amd.h.  It is built for gfx950 only, in place, so the .so travels with the
+repository snapshot to the GPU box.
+"""
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "librtamd.so")
+SOURCES = ["rt_host.cpp", "rt_device.hip"]
+HEADERS = ["rt_math.h", "rt_internal.h", os.path.join("..", "..", "include", "rt_amd.h")]
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -ffp-contract=off + IEEE div/sqrt (hipcc's default) keep the kernels' float results
+# bit-identical to the reference's evaluation order.
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+         "-Wall", "-Wno-unused-function"]
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.abspath(__file__)]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False):
+    if not force and not _stale():
+        return LIB
+    cmd = [HIPCC] + FLAGS + ["-o", LIB + ".tmp"] + [os.path.join(CSRC, f) for f in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,1119 @@
+// rt_device.hip -- gfx950 kernels and the device half of the C-ABI.
+//
+// Hot path: Renderer::Tick -> Camera::GetPrimaryRay -> Renderer::Trace
+// -> Scene::IntersectBVH / IsOccluded -> Primitive::Intersect / Hit, plus
+// NextEventDirectIllumination, the Diffuse / Mirror / Dielectric / Checkerboard / Light
+// materials, the sky lookup, the running-average accumulator and the RGB8 pack -- all in
+// ONE kernel launch per frame (k_render).  Launch shape: 256-thread workgroups of four
+// wave64s, one wave per 8x8 screen tile (the reference's PACKET_SIZE 64 / SQRT_PACKET_SIZE 8,
+// Ray.h:3-5), one lane per pixel.  No MFMA: this is branchy scalar fp32.
+//
+// Device scene layout in HBM (built once by rt_scene_create):
+//   nodes  : the reference's 32-byte BVHNode array (root 0, node 1 unused, sibling pairs
+//            64-byte aligned) with (leftFirst, count) replaced by one packed word
+//            (leftFirst << 8 | count) so a 64-byte sibling-pair load carries everything
+//            the traversal needs;
+//   prims  : leaf order (primitiveIndices applied), 48 B per slot: triangle A, B-A, C-A
+//            (host-computed, bit-identical to the reference's per-test subtraction) and
+//            the original primitive id -- no index indirection in the leaf loop;
+//   shade  : per primitive id, 32 B: geometric normal (triangles, host-computed with the
+//            reference's normalize(cross(..))), sphere centre / 1/r, material id;
+//   per-lane traversal stack: LDS, [depth][256 lanes] u32, conflict-free.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rt_internal.h"
+
+namespace rt {
+
+enum : uint32_t { T_TRI = 4, T_SPH = 0, T_PLANE = 1 };
+enum : int { F_DIFFUSE = 0, F_SPECULAR = 1, F_MIX = 2, F_DIELECTRIC = 3, F_LIGHT = 4 };
+
+struct DevMaterial {
+    int kind, flag;
+    float c0[3], c1[3];
+    float ior, diffuse, specular, pad;
+};
+
+struct SceneView {
+    const float4 *__restrict__ nodes;   // 2 float4 per node
+    const float4 *__restrict__ prims;   // 3 float4 per leaf slot
+    const float4 *__restrict__ shade;   // 2 float4 per primitive id
+    const DevMaterial *__restrict__ mats;
+    const uint32_t *__restrict__ sky;
+    uint32_t sky_w, sky_h;
+    int sky_const;
+    float sky_rgb[3];
+    float light_M[12];                  // prim 0 Transform rows 0..2 (Translate)
+    float light_c[3];
+    float light_r, light_r2, light_invr;
+    int light_mat;
+    uint32_t root_word;
+};
+
+struct FrameArgs {
+    float cam_pos[3], cam_tl[3], cam_tr[3], cam_bl[3];
+    float lens, rw, rh;
+    uint32_t W, H, spp, depth, frame, reset;
+    uint32_t shard, nshards, tiles_x, ntiles_local;
+    int packed_out;
+    float4 *acc;
+    uint32_t *out;
+    unsigned long long *counters;       // [0] shadow rays, [1] bounce rays
+};
+
+struct DRay {
+    f3 O, D, rD;
+    float t;
+    int obj;
+    int inside;
+    float u, v;
+};
+
+__device__ __forceinline__ DRay make_ray(f3 O, f3 D, float t) {   // Ray.h:9-16
+    DRay r;
+    r.O = O; r.D = D; r.t = t; r.obj = -1; r.inside = 0; r.u = 0.0f; r.v = 0.0f;
+    r.rD = mk(1 / D.x, 1 / D.y, 1 / D.z);
+    return r;
+}
+
+// correctly rounded float transcendentals (double evaluation, matching the oracle)
+__device__ __forceinline__ float cr_cos(float x) { return (float)cos((double)x); }
+__device__ __forceinline__ float cr_sin(float x) { return (float)sin((double)x); }
+__device__ __forceinline__ float cr_exp(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float cr_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+__device__ __forceinline__ float cr_acos(float x) { return (float)acos((double)x); }
+__device__ __forceinline__ float cr_asin(float x) { return (float)asin((double)x); }
+
+// float -> uint the way the reference's x86-64 build converts: (uint32)(int64)trunc(f)
+__device__ __forceinline__ uint32_t f2u_wrap(float f) {
+    if (!(f == f) || f >= 9.2e18f || f <= -9.2e18f) return 0u;
+    return (uint32_t)(long long)f;
+}
+
+// ------------------------------------------------------------------ slab tests (scene.h:414-450)
+__device__ __forceinline__ float slab_dist(const DRay &r, float4 a, float4 b) {
+    float tx1 = (a.x - r.O.x) * r.rD.x, tx2 = (a.w - r.O.x) * r.rD.x;
+    float tmn = smin(tx1, tx2), tmx = smax(tx1, tx2);
+    float ty1 = (a.y - r.O.y) * r.rD.y, ty2 = (b.x - r.O.y) * r.rD.y;
+    tmn = smax(tmn, smin(ty1, ty2)); tmx = smin(tmx, smax(ty1, ty2));
+    float tz1 = (a.z - r.O.z) * r.rD.z, tz2 = (b.y - r.O.z) * r.rD.z;
+    tmn = smax(tmn, smin(tz1, tz2)); tmx = smin(tmx, smax(tz1, tz2));
+    return (tmx >= tmn && tmn < r.t && tmx > 0) ? tmn : 1e30f;
+}
+__device__ __forceinline__ bool slab_hit(const DRay &r, float4 a, float4 b) {
+    float tx1 = (a.x - r.O.x) * r.rD.x, tx2 = (a.w - r.O.x) * r.rD.x;
+    float tmn = smin(tx1, tx2), tmx = smax(tx1, tx2);
+    float ty1 = (a.y - r.O.y) * r.rD.y, ty2 = (b.x - r.O.y) * r.rD.y;
+    tmn = smax(tmn, smin(ty1, ty2)); tmx = smin(tmx, smax(ty1, ty2));
+    float tz1 = (a.z - r.O.z) * r.rD.z, tz2 = (b.y - r.O.z) * r.rD.z;
+    tmn = smax(tmn, smin(tz1, tz2)); tmx = smin(tmx, smax(tz1, tz2));
+    return tmx >= tmn && tmn < r.t && tmx > 0;
+}
+
+// ------------------------------------------------------------------ primitive tests (Primitive.h:64-279)
+__device__ __forceinline__ void prim_intersect(const SceneView &S, uint32_t k, DRay &r) {
+    float4 p0 = S.prims[3 * k], p1 = S.prims[3 * k + 1];
+    uint32_t type = __float_as_uint(p1.w);
+    int id = __float_as_int(p0.w);
+    if (type == T_TRI) {
+        float4 p2 = S.prims[3 * k + 2];
+        f3 A = mk(p0.x, p0.y, p0.z), AB = mk(p1.x, p1.y, p1.z), AC = mk(p2.x, p2.y, p2.z);
+        float denom = dot(cross(r.D, AC), AB);
+        if (fabsf(denom) < kDENOM_EPS) return;
+        f3 AO = r.O - A;
+        float u = dot(cross(-r.D, AO), AC) / denom;
+        if (u < 0 || u > 1) return;
+        float v = dot(cross(-r.D, AB), AO) / denom;
+        if (v < 0 || u + v > 1) return;
+        float t = dot(cross(AO, AB), AC) / denom;
+        if (t < r.t && t > kEPS) { r.t = t; r.obj = id; r.u = u; r.v = v; }
+    } else if (type == T_SPH) {
+        f3 oc = r.O - mk(p0.x, p0.y, p0.z);
+        float b = dot(oc, r.D);
+        float c = dot(oc, oc) - p1.x;
+        float d = b * b - c;
+        if (d <= 0) return;
+        d = sqrtf(d);
+        float t = -b - d;
+        if (!(t < r.t && t > kEPS)) {
+            t = d - b;
+            if (!(t < r.t && t > kEPS)) return;
+        }
+        r.t = t; r.obj = id;            // u, v filled in after traversal (finish_uv)
+    } else {
+        f3 N = mk(p0.x, p0.y, p0.z);
+        float t = -(dot(r.O, N) + p1.x) / (dot(r.D, N));
+        if (t < r.t && t > kEPS) { r.t = t; r.obj = id; }
+    }
+}
+
+__device__ __forceinline__ bool prim_hit(const SceneView &S, uint32_t k, const DRay &r) {
+    float4 p0 = S.prims[3 * k], p1 = S.prims[3 * k + 1];
+    uint32_t type = __float_as_uint(p1.w);
+    if (type == T_TRI) {
+        float4 p2 = S.prims[3 * k + 2];
+        f3 A = mk(p0.x, p0.y, p0.z), AB = mk(p1.x, p1.y, p1.z), AC = mk(p2.x, p2.y, p2.z);
+        float denom = dot(cross(r.D, AC), AB);
+        if (fabsf(denom) < kDENOM_EPS) return false;
+        f3 AO = r.O - A;
+        float u = dot(cross(-r.D, AO), AC) / denom;
+        if (u < 0 || u > 1) return false;
+        float v = dot(cross(-r.D, AB), AO) / denom;
+        if (v < 0 || u + v > 1) return false;
+        float t = dot(cross(AO, AB), AC) / denom;
+        return t < r.t && t > kEPS;
+    } else if (type == T_SPH) {
+        f3 oc = r.O - mk(p0.x, p0.y, p0.z);
+        float b = dot(oc, r.D);
+        float c = dot(oc, oc) - p1.x;
+        float d = b * b - c;
+        if (d <= 0) return false;
+        d = sqrtf(d);
+        float t = -b - d;
+        if (t < r.t && t > kEPS) return true;
+        t = d - b;
+        return t < r.t && t > kEPS;
+    } else {
+        f3 N = mk(p0.x, p0.y, p0.z);
+        float t = -(dot(r.O, N) + p1.x) / (dot(r.D, N));
+        return t < r.t && t > kEPS;
+    }
+}
+
+// u, v of a sphere / plane hit, evaluated once for the final hit: identical to the
+// reference's evaluation at acceptance time (same t, same centre).
+__device__ __forceinline__ void finish_uv(const SceneView &S, DRay &r) {
+    if (r.obj < 0) return;
+    float4 s0 = S.shade[2 * r.obj], s1 = S.shade[2 * r.obj + 1];
+    uint32_t type = __float_as_uint(s1.x);
+    f3 I = r.O + r.t * r.D;
+    if (type == T_SPH) {
+        f3 cToI = normalize(I - mk(s0.x, s0.y, s0.z));
+        r.u = 0.5f - cr_atan2(cToI.z, cToI.x) * kINV2PI;
+        r.v = 0.5f - cr_asin(cToI.y) * kINVPI;
+    } else if (type == T_PLANE) {
+        if (s0.x < kFLT_EPSILON && s0.y < kFLT_EPSILON) { r.u = I.x; r.v = -I.y; }
+        else if (s0.x < kFLT_EPSILON && s0.z < kFLT_EPSILON) { r.u = I.x; r.v = -I.z; }
+        else if (s0.y < kFLT_EPSILON && s0.z < kFLT_EPSILON) { r.u = I.y; r.v = -I.z; }
+    }
+}
+
+// ------------------------------------------------------------------ traversal (scene.h:285-320, 452-487)
+// stk points at this lane's column of the LDS stack; entry i lives at stk[i * 256].
+__device__ __forceinline__ void closest_hit(const SceneView &S, DRay &r, uint32_t *stk) {
+    uint32_t word = S.root_word;
+    int sp = 0;
+    for (;;) {
+        uint32_t cnt = word & 0xffu, lf = word >> 8;
+        if (cnt) {
+            for (uint32_t k = lf; k < lf + cnt; ++k) prim_intersect(S, k, r);
+            if (sp == 0) break;
+            word = stk[--sp * 256];
+            continue;
+        }
+        const float4 *q = S.nodes + 2 * lf;
+        float4 a0 = q[0], b0 = q[1], a1 = q[2], b1 = q[3];
+        float d1 = slab_dist(r, a0, b0), d2 = slab_dist(r, a1, b1);
+        uint32_t w1 = __float_as_uint(b0.z), w2 = __float_as_uint(b1.z);
+        if (d1 > d2) { float td = d1; d1 = d2; d2 = td; uint32_t tw = w1; w1 = w2; w2 = tw; }
+        if (d1 == 1e30f) {
+            if (sp == 0) break;
+            word = stk[--sp * 256];
+        } else {
+            word = w1;
+            if (d2 != 1e30f) stk[sp++ * 256] = w2;
+        }
+    }
+}
+
+__device__ __forceinline__ bool occluded(const SceneView &S, const DRay &r, uint32_t *stk) {
+    uint32_t word = S.root_word;
+    int sp = 0;
+    for (;;) {
+        uint32_t cnt = word & 0xffu, lf = word >> 8;
+        if (cnt) {
+            for (uint32_t k = lf; k < lf + cnt; ++k)
+                if (prim_hit(S, k, r)) return true;
+            if (sp == 0) return false;
+            word = stk[--sp * 256];
+            continue;
+        }
+        const float4 *q = S.nodes + 2 * lf;
+        float4 a0 = q[0], b0 = q[1], a1 = q[2], b1 = q[3];
+        bool h1 = slab_hit(r, a0, b0), h2 = slab_hit(r, a1, b1);
+        uint32_t w1 = __float_as_uint(b0.z), w2 = __float_as_uint(b1.z);
+        if (h1 && h2) { word = w1; stk[sp++ * 256] = w2; }
+        else if (!(h1 || h2)) { if (sp == 0) return false; word = stk[--sp * 256]; }
+        else word = h1 ? w1 : w2;
+    }
+}
+
+// ------------------------------------------------------------------ shading
+__device__ __forceinline__ f3 sky_color(const SceneView &S, f3 D) {   // renderer.h:15-22
+    if (S.sky_const) return mk(S.sky_rgb[0], S.sky_rgb[1], S.sky_rgb[2]);
+    uint32_t u = f2u_wrap((float)S.sky_w * cr_atan2(D.z, D.x) * kINV2PI - 0.5f);
+    uint32_t v = f2u_wrap((float)S.sky_h * cr_acos(D.y) * kINVPI - 0.5f);
+    uint32_t p = S.sky[(u & (S.sky_w - 1)) + (v & (S.sky_h - 1)) * S.sky_w];
+    return mk((float)((p >> 16) & 255), (float)((p >> 8) & 255), (float)(p & 255)) * kSKY;
+}
+
+// ObjectMaterial::DiffuseReflection + mapToNormalAxis (ObjectMaterial.h:18-53)
+__device__ __forceinline__ f3 diffuse_dir(f3 N, uint32_t &seed) {
+    float r0 = rnd_f(seed), r1 = rnd_f(seed);
+    float r = sqrtf(r0), theta = kTWOPI * r1;
+    float x = r * cr_cos(theta), y = r * cr_sin(theta), z = sqrtf(1 - r0);
+    f3 a0 = mk(0.0f, -1.0f, 0.0f), a1 = mk(-1.0f, 0.0f, 0.0f);
+    if (N.z + 1.0f > kFLT_EPSILON) {
+        float a = 1.0f / (1.0f + N.z);
+        float b = -N.x * N.y * a;
+        a0 = mk(1.0f - N.x * N.x * a, b, -N.x);
+        a1 = mk(b, 1.0f - N.y * N.y * a, -N.y);
+    }
+    return normalize(x * a0 + y * a1 + z * N);
+}
+
+__device__ __forceinline__ float fresnel(float n1, float n2, float cost, float cosi) {   // ObjectMaterial.h:55-60
+    float s = (n1 * cosi - n2 * cost) / (n1 * cosi + n2 * cost);
+    float p = (n1 * cost - n2 * cosi) / (n1 * cost + n2 * cosi);
+    return 0.5f * ((s * s) + (p * p));
+}
+
+// ObjectMaterial::scatter overrides.  With last = true the bounce ray is never traced
+// (Trace(.., depth 0) returns 0), so only the RNG draws and the specular flag are kept.
+__device__ __forceinline__ bool scatter(const DevMaterial &m, const DRay &in, f3 I, f3 N, DRay &out, uint32_t &seed,
+                                        bool last) {
+    switch (m.kind) {
+    case RT_DIFFUSE:                                                   // Diffuse.h:16-19
+        if (last) { rnd_u(seed); rnd_u(seed); }
+        else out = make_ray(I, diffuse_dir(N, seed), 1e34f);
+        return false;
+    case RT_MIRROR:                                                    // Mirror.h:16-19
+        if (!last) out = make_ray(I, normalize(reflect(in.D, N)), 1e34f);
+        return true;
+    case RT_DIELECTRIC: {                                              // Dielectric.h:23-54
+        float n1 = 1, n2 = m.ior;
+        float n12 = n1 / n2;
+        float cosi = dot(N, in.D);
+        if (in.inside) n12 = 1 / n12;
+        float k = 1 - (n12 * n12) * (1 - (cosi * cosi));
+        if (k < 0) {
+            if (!last) { out = make_ray(I, normalize(reflect(in.D, N)), 1e34f); out.inside = 1; }
+        } else {
+            float Fr = 0;
+            if (!in.inside) {
+                float sini = length(cross(N, in.D));
+                float sq = n12 * sini;
+                float cost = sqrtf(1 - sq * sq);
+                Fr = fresnel(n1, n2, cost, -cosi);
+            }
+            if (Fr > kFLT_EPSILON && rnd_f(seed) < Fr) {
+                if (!last) out = make_ray(I, normalize(reflect(in.D, N)), 1e34f);
+            } else if (!last) {
+                f3 T = normalize(n12 * in.D - (n12 * cosi + sqrtf(k)) * N);
+                out = make_ray(I, T, 1e34f);
+                out.inside = !in.inside;
+            }
+        }
+        return true;
+    }
+    case RT_LIGHT:
+        return false;
+    default:                                                           // Checkerboard.h:39-58
+        if (m.diffuse < kFLT_EPSILON) {
+            if (!last) out = make_ray(I, normalize(reflect(in.D, N)), 1e34f);
+            return true;
+        }
+        if (m.specular < kFLT_EPSILON) {
+            if (last) { rnd_u(seed); rnd_u(seed); }
+            else out = make_ray(I, diffuse_dir(N, seed), 1e34f);
+            return false;
+        }
+        if (rnd_f(seed) < m.specular) {
+            if (!last) out = make_ray(I, normalize(reflect(in.D, N)), 1e34f);
+            return true;
+        }
+        if (last) { rnd_u(seed); rnd_u(seed); }
+        else out = make_ray(I, diffuse_dir(N, seed), 1e34f);
+        return false;
+    }
+}
+
+__device__ __forceinline__ f3 mat_color(const DevMaterial &m, const DRay &in, f3 I) {
+    if (m.kind == RT_DIELECTRIC) {                                     // Dielectric.h:12-21
+        f3 c = mk(1, 1, 1);
+        if (in.inside) { c.x = cr_exp(-m.c0[0] * in.t); c.y = cr_exp(-m.c0[1] * in.t); c.z = cr_exp(-m.c0[2] * in.t); }
+        return c;
+    }
+    if (m.kind == RT_CHECKERBOARD) {                                   // Checkerboard.h:28-37
+        bool ex = abs(((int)floorf(I.x)) % 2) == 0;
+        bool ez = abs(((int)floorf(I.z)) % 2) == 0;
+        return ex == ez ? mk(m.c0[0], m.c0[1], m.c0[2]) : mk(m.c1[0], m.c1[1], m.c1[2]);
+    }
+    return mk(m.c0[0], m.c0[1], m.c0[2]);
+}
+
+// Renderer::NextEventDirectIllumination, renderer.h:44-75 (light = prim 0, a sphere)
+__device__ __forceinline__ f3 nee(const SceneView &S, f3 I, f3 N, f3 BRDF, uint32_t &seed, uint32_t *stk,
+                                  uint32_t &nshadow) {
+    f3 pt = mk(1, 1, 1);                                               // GetRandomPoint, Primitive.h:394-402
+    while (dot(pt, pt) > 1) {
+        float x = rnd_f(seed) * 2.0f - 1.0f;
+        float y = rnd_f(seed) * 2.0f - 1.0f;
+        float z = rnd_f(seed) * 2.0f - 1.0f;
+        pt = mk(x, y, z);
+    }
+    f3 Il = tpos(S.light_M, normalize(pt) * S.light_r);
+    float area = 4.0f * kPI * S.light_r2;                              // GetArea, Primitive.h:452
+    f3 L = Il - I;
+    float dist = length(L);
+    L = L / dist;
+    f3 Nl = (Il - mk(S.light_c[0], S.light_c[1], S.light_c[2])) * S.light_invr;
+    if (dot(Nl, L) > 0) Nl = -Nl;                                      // Scene::GetNormal flip
+    float dotNL = dot(N, L), dotNlL = dot(Nl, -L);
+    f3 Ld = mk(0, 0, 0);
+    if (dotNL > 0 && dotNlL > 0) {
+        DRay sh = make_ray(I, L, dist - 2.0f * kEPS);
+        ++nshadow;
+        if (!occluded(S, sh, stk)) {
+            float solid = (dotNlL * area) / (dist * dist);
+            float lightPDF = 1.0f / solid;
+            const DevMaterial &lm = S.mats[S.light_mat];
+            Ld = (mk(lm.c0[0], lm.c0[1], lm.c0[2]) * BRDF) * (dotNL / lightPDF);
+        }
+    }
+    return Ld;
+}
+
+// Renderer::Trace (renderer.cpp:17-72) as a loop.  The recursion's result
+// BRDF * ((Trace * dot) / PDF) + Ld is folded innermost-first from per-level records,
+// so the float evaluation order is the reference's.
+template <int MAXD>
+__device__ f3 trace_path(const SceneView &S, DRay ray, int depth, uint32_t &seed, uint32_t *stk, uint32_t &nshadow,
+                         uint32_t &nbounce) {
+    f3 lv_mul[MAXD], lv_add[MAXD];
+    float lv_c[MAXD];
+    bool lv_diff[MAXD];
+    int levels = 0;
+    f3 term = mk(0, 0, 0);
+    bool lastSpec = true;
+    for (int d = depth; d > 0 && levels < MAXD; --d) {
+        if (d != depth) ++nbounce;
+        closest_hit(S, ray, stk);
+        if (ray.obj == -1) { term = sky_color(S, ray.D); break; }
+        f3 I = ray.O + ray.t * ray.D;
+        float4 s0 = S.shade[2 * ray.obj], s1 = S.shade[2 * ray.obj + 1];
+        uint32_t ptype = __float_as_uint(s1.x);
+        f3 N = ptype == T_SPH ? (I - mk(s0.x, s0.y, s0.z)) * s1.y : mk(s0.x, s0.y, s0.z);
+        if (dot(N, ray.D) > 0) N = -N;                                 // Scene::GetNormal
+        const DevMaterial &m = S.mats[__float_as_int(s0.w)];
+        if (m.flag == F_LIGHT) { term = lastSpec ? mk(m.c0[0], m.c0[1], m.c0[2]) : mk(0, 0, 0); break; }
+        const bool last = (d == 1);
+        DRay out;
+        bool spec = scatter(m, ray, I, N, out, seed, last);
+        f3 albedo = mat_color(m, ray, I);
+        if (m.flag == F_DIFFUSE || (m.flag == F_MIX && !spec)) {
+            f3 BRDF = albedo * kINVPI;
+            lv_add[levels] = nee(S, I, N, BRDF, seed, stk, nshadow);
+            lv_mul[levels] = BRDF;
+            lv_c[levels] = last ? 0.0f : dot(N, out.D);
+            lv_diff[levels] = true;
+        } else {
+            lv_mul[levels] = albedo;
+            lv_add[levels] = mk(0, 0, 0);
+            lv_c[levels] = 0.0f;
+            lv_diff[levels] = false;
+        }
+        ++levels;
+        if (last) break;
+        ray = out;
+        lastSpec = spec;
+    }
+    f3 r = term;
+    for (int k = levels - 1; k >= 0; --k)
+        r = lv_diff[k] ? lv_mul[k] * ((r * lv_c[k]) / kINV2PI) + lv_add[k] : lv_mul[k] * r;
+    return r;
+}
+
+// Camera::GetPrimaryRay (camera.h:43-52) + randomInUnitDisk (20-26)
+__device__ __forceinline__ DRay primary_ray(const FrameArgs &F, uint32_t x, uint32_t y, uint32_t &seed) {
+    float u = (float)x * F.rw + rnd_f(seed) * F.rw;
+    float v = (float)y * F.rh + rnd_f(seed) * F.rh;
+    f3 p;
+    for (;;) {
+        float px = rnd_f(seed) * 2.0f - 1.0f;
+        float py = rnd_f(seed) * 2.0f - 1.0f;
+        p = mk(px, py, 0);
+        if (!(dot(p, p) >= 1)) break;
+    }
+    f3 rd = F.lens * p;
+    f3 offset = mk(u * rd.x, v * rd.y, 0);
+    f3 pos = mk(F.cam_pos[0], F.cam_pos[1], F.cam_pos[2]);
+    f3 tl = mk(F.cam_tl[0], F.cam_tl[1], F.cam_tl[2]);
+    f3 tr = mk(F.cam_tr[0], F.cam_tr[1], F.cam_tr[2]);
+    f3 bl = mk(F.cam_bl[0], F.cam_bl[1], F.cam_bl[2]);
+    f3 P = tl + u * (tr - tl) + v * (bl - tl);
+    return make_ray(pos + offset, normalize(P - pos - offset), 1e34f);
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// RGBF32_to_RGB8, template/precomp.h:441-444
+__device__ __forceinline__ uint32_t pack_rgb8(float4 a) {
+    uint32_t r = f2u_wrap(255.0f * smin(1.0f, a.x));
+    uint32_t g = f2u_wrap(255.0f * smin(1.0f, a.y));
+    uint32_t b = f2u_wrap(255.0f * smin(1.0f, a.z));
+    return (r << 16) + (g << 8) + b;
+}
+
+// ------------------------------------------------------------------ kernels
+// One frame (Renderer::Tick, renderer.cpp:200-309): per pixel spp x Trace, running
+// average into the accumulator, RGB8 pack.  Wave w of workgroup b owns screen tile
+// (b*4 + w) * nshards + shard.
+template <int MAXD>
+__global__ __launch_bounds__(256) void k_render(SceneView S, FrameArgs F) {
+    extern __shared__ uint32_t lds_stack[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t local_tile = blockIdx.x * 4u + (tid >> 6);
+    if (local_tile >= F.ntiles_local) return;
+    const uint32_t tile = local_tile * F.nshards + F.shard;
+    const uint32_t x = (tile % F.tiles_x) * 8u + (lane & 7u), y = (tile / F.tiles_x) * 8u + (lane >> 3);
+    uint32_t nshadow = 0, nbounce = 0;
+    if (x < F.W && y < F.H) {
+        uint32_t *stk = lds_stack + tid;
+        const uint32_t px = x + y * F.W;
+        f3 sum = mk(0, 0, 0);
+        for (uint32_t s = 0; s < F.spp; ++s) {
+            uint32_t seed = init_seed(px + F.W * F.H * (s + F.spp * F.frame));
+            DRay ray = primary_ray(F, x, y, seed);
+            sum = sum + trace_path<MAXD>(S, ray, (int)F.depth, seed, stk, nshadow, nbounce);
+        }
+        f3 res = (1.0f / (float)F.spp) * sum;
+        float4 a = F.reset ? make_float4(0, 0, 0, 0) : F.acc[px];
+        a.w += 1;                                                      // renderer.cpp:237-240
+        const float w = a.w, inv = 1.0f / w;
+        a = make_float4(a.x + inv * (res.x - a.x), a.y + inv * (res.y - a.y), a.z + inv * (res.z - a.z),
+                        a.w + inv * (w - a.w));
+        F.acc[px] = a;
+        const uint32_t rgb = pack_rgb8(a);
+        if (F.packed_out) F.out[local_tile * 64u + lane] = rgb;
+        else F.out[px] = rgb;
+    }
+    nshadow = wave_sum(nshadow);
+    nbounce = wave_sum(nbounce);
+    if (lane == 0) {
+        if (nshadow) atomicAdd(&F.counters[0], (unsigned long long)nshadow);
+        if (nbounce) atomicAdd(&F.counters[1], (unsigned long long)nbounce);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_intersect(SceneView S, const rt_ray *__restrict__ rays, rt_hit *__restrict__ hits,
+                                                   uint32_t n) {
+    extern __shared__ uint32_t lds_stack[];
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    rt_ray q = rays[i];
+    DRay r = make_ray(mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), q.tmax);
+    closest_hit(S, r, lds_stack + threadIdx.x);
+    finish_uv(S, r);
+    rt_hit h;
+    h.t = r.t; h.obj = r.obj; h.u = r.u; h.v = r.v;
+    hits[i] = h;
+}
+
+__global__ __launch_bounds__(256) void k_occluded(SceneView S, const rt_ray *__restrict__ rays, uint8_t *__restrict__ out,
+                                                  uint32_t n) {
+    extern __shared__ uint32_t lds_stack[];
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    rt_ray q = rays[i];
+    DRay r = make_ray(mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), q.tmax);
+    out[i] = occluded(S, r, lds_stack + threadIdx.x) ? 1 : 0;
+}
+
+// rank-0 side of the per-frame gather: packed shard tiles -> row-major frame
+__global__ __launch_bounds__(256) void k_assemble(const uint32_t *__restrict__ gathered, uint32_t cap, uint32_t nshards,
+                                                  uint32_t tiles_x, uint32_t ntiles, uint32_t W, uint32_t H,
+                                                  uint32_t *__restrict__ out) {
+    const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    if (tile >= ntiles) return;
+    const uint32_t x = (tile % tiles_x) * 8u + (lane & 7u), y = (tile / tiles_x) * 8u + (lane >> 3);
+    if (x >= W || y >= H) return;
+    const uint32_t shard = tile % nshards, local = tile / nshards;
+    out[x + y * W] = gathered[(size_t)shard * cap + local * 64u + lane];
+}
+
+}  // namespace rt
+
+// ====================================================================== host side
+using namespace rt;
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(e_ == hipErrorNoBinaryForGpu || e_ == hipErrorInvalidDeviceFunction    \
+                            ? RT_ERR_NO_DEVICE : RT_ERR_HIP,                                   \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                   \
+    } while (0)
+
+struct rt_scene {
+    int device = 0;
+    SceneView view{};
+    Bvh bvh;
+    uint32_t num_prims = 0;
+    uint32_t stack_depth = 0;   // LDS stack entries per lane
+    void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
+    void *d_scratch = nullptr;  // staging for the host-pointer batched calls
+    size_t scratch_bytes = 0;
+    hipStream_t stream = nullptr;
+};
+
+struct rt_renderer {
+    rt_scene *scene = nullptr;
+    uint32_t W = 0, H = 0;
+    float4 *d_acc = nullptr;
+    unsigned long long *d_counters = nullptr;
+    uint32_t *d_rgb = nullptr;   // staging frame for rt_render_frame_host
+    uint64_t primary = 0, frames = 0;
+    hipStream_t stream = nullptr;
+};
+
+namespace {
+
+inline float ubits(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+inline float ibits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
+
+uint32_t pick_stack(uint32_t depth) {   // entries needed <= tree depth; round up to 8
+    uint32_t need = depth < 2 ? 2 : depth;
+    return (need + 7u) & ~7u;
+}
+
+int material_flag(const rt_material &m, float diffuse, float specular) {   // getFlag overrides
+    switch (m.kind) {
+    case RT_DIFFUSE: return F_DIFFUSE;
+    case RT_MIRROR: return F_SPECULAR;
+    case RT_DIELECTRIC: return F_DIELECTRIC;
+    case RT_LIGHT: return F_LIGHT;
+    default:
+        if (diffuse < kFLT_EPSILON) return F_SPECULAR;
+        if (specular < kFLT_EPSILON) return F_DIFFUSE;
+        return F_MIX;
+    }
+}
+
+int validate_bvh(const Bvh &b, uint32_t n) {
+    if (b.nodes_used < 2 || b.nodes_used > b.nodes.size()) return fail(RT_ERR_INVALID, "BVH node count out of range");
+    std::vector<uint8_t> seen(n, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (b.indices[i] >= n || seen[b.indices[i]]) return fail(RT_ERR_INVALID, "BVH indices are not a permutation");
+        seen[b.indices[i]] = 1;
+    }
+    // walk from the root: children in range, leaves inside the index array
+    std::vector<uint32_t> st{0};
+    size_t visits = 0;
+    while (!st.empty()) {
+        uint32_t k = st.back();
+        st.pop_back();
+        if (++visits > 2 * (size_t)b.nodes_used) return fail(RT_ERR_INVALID, "BVH has a cycle");
+        const Node &nd = b.nodes[k];
+        if (nd.count > 0) {
+            if ((uint64_t)nd.leftFirst + nd.count > n) return fail(RT_ERR_INVALID, "BVH leaf outside the index array");
+            continue;
+        }
+        if (nd.leftFirst < 2 || nd.leftFirst + 1 >= b.nodes_used || (nd.leftFirst & 1u))
+            return fail(RT_ERR_INVALID, "BVH child pair out of range / misaligned");
+        st.push_back(nd.leftFirst);
+        st.push_back(nd.leftFirst + 1);
+    }
+    return RT_OK;
+}
+
+void free_scene(rt_scene *s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    void *ptrs[] = {s->d_nodes, s->d_prims, s->d_shade, s->d_mats, s->d_sky, s->d_scratch};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+}
+
+template <typename T>
+int upload(void **dst, const std::vector<T> &src) {
+    HIP_TRY(hipMalloc(dst, std::max<size_t>(sizeof(T) * src.size(), 16)));
+    if (!src.empty()) HIP_TRY(hipMemcpy(*dst, src.data(), sizeof(T) * src.size(), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+int ensure_device(int device) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        return fail(RT_ERR_NO_DEVICE, "no HIP device visible: the MI355X path has no CPU fallback");
+    if (device < 0 || device >= count) return fail(RT_ERR_INVALID, "device index out of range");
+    HIP_TRY(hipSetDevice(device));
+    return RT_OK;
+}
+
+int scene_create(const rt_scene_desc *d, rt_scene **out) {
+    if (!d || !out || !d->prims || d->num_prims == 0 || !d->materials || d->num_materials == 0)
+        return fail(RT_ERR_INVALID, "rt_scene_create: empty or null description");
+    *out = nullptr;
+    const uint32_t n = d->num_prims;
+    if (n >= (1u << 24)) return fail(RT_ERR_UNSUPPORTED, "more than 2^24 primitives");
+    for (uint32_t i = 0; i < n; ++i) {
+        const rt_prim &p = d->prims[i];
+        if (p.type != RT_SPHERE && p.type != RT_PLANE && p.type != RT_TRIANGLE)
+            return fail(RT_ERR_INVALID, "primitive " + std::to_string(i) + ": unknown type");
+        if (p.material < 0 || (uint32_t)p.material >= d->num_materials)
+            return fail(RT_ERR_INVALID, "primitive " + std::to_string(i) + ": material out of range");
+    }
+    if (d->prims[0].type != RT_SPHERE)
+        return fail(RT_ERR_UNSUPPORTED, "primitive 0 must be the light sphere (Scene::GetRandomLight returns 0)");
+    if (d->sky_pixels) {
+        uint32_t w = d->sky_width, h = d->sky_height;
+        if (!w || !h || (w & (w - 1)) || (h & (h - 1)))
+            return fail(RT_ERR_INVALID, "sky texture must have power-of-two sides (renderer.h:18)");
+    }
+    int rc = ensure_device(d->device);
+    if (rc != RT_OK) return rc;
+
+    rt_scene *s = new rt_scene();
+    s->device = d->device;
+    s->num_prims = n;
+    // ---- BVH: prebuilt (validated) or built here
+    if (d->bvh_nodes) {
+        if (!d->bvh_indices || d->bvh_num_nodes < 2) { delete s; return fail(RT_ERR_INVALID, "prebuilt BVH incomplete"); }
+        s->bvh.nodes.resize(d->bvh_num_nodes);
+        std::memcpy(s->bvh.nodes.data(), d->bvh_nodes, sizeof(Node) * d->bvh_num_nodes);
+        s->bvh.indices.assign(d->bvh_indices, d->bvh_indices + n);
+        s->bvh.nodes_used = d->bvh_num_nodes;
+        if ((rc = validate_bvh(s->bvh, n)) != RT_OK) { delete s; return rc; }
+        // depth + widest leaf
+        // depth as Scene::maxDepthBVH (template/scene.h:144-154): interior levels, root leaf = 1
+        std::vector<std::pair<uint32_t, uint32_t>> st{{0, 0}};
+        while (!st.empty()) {
+            auto [k, dd] = st.back();
+            st.pop_back();
+            const Node &nd = s->bvh.nodes[k];
+            if (nd.count > 0) {
+                s->bvh.max_leaf = std::max(s->bvh.max_leaf, nd.count);
+                s->bvh.depth = std::max(s->bvh.depth, k == 0 ? 1u : dd);
+                continue;
+            }
+            st.push_back({nd.leftFirst, dd + 1});
+            st.push_back({nd.leftFirst + 1, dd + 1});
+        }
+    } else if ((rc = build_bvh(d->prims, n, s->bvh)) != RT_OK) {
+        delete s;
+        return rc;
+    }
+    if (s->bvh.max_leaf > 255) { delete s; return fail(RT_ERR_UNSUPPORTED, "BVH leaf with more than 255 primitives"); }
+    if (s->bvh.depth > 64) { delete s; return fail(RT_ERR_UNSUPPORTED, "BVH deeper than 64 (the reference's stack[64])"); }
+    s->stack_depth = pick_stack(s->bvh.depth);
+
+    // ---- device node array: packed (leftFirst << 8 | count) word in b.z
+    std::vector<float4> nodes(2 * (size_t)s->bvh.nodes_used);
+    for (uint32_t i = 0; i < s->bvh.nodes_used; ++i) {
+        const Node &nd = s->bvh.nodes[i];
+        uint32_t word = (nd.leftFirst << 8) | nd.count;
+        nodes[2 * i] = make_float4(nd.mn[0], nd.mn[1], nd.mn[2], nd.mx[0]);
+        nodes[2 * i + 1] = make_float4(nd.mx[1], nd.mx[2], ubits(word), 0.0f);
+    }
+    // ---- leaf-order primitive records and per-id shading records
+    static const float I16[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    std::vector<float4> prims(3 * (size_t)n), shade(2 * (size_t)n);
+    for (uint32_t id = 0; id < n; ++id) {
+        const rt_prim &p = d->prims[id];
+        float4 s0, s1 = make_float4(ubits((uint32_t)p.type), 0, 0, 0);
+        if (p.type == RT_TRIANGLE) {
+            f3 d0 = mk(p.v[0], p.v[1], p.v[2]), d1 = mk(p.v[3], p.v[4], p.v[5]), d2 = mk(p.v[6], p.v[7], p.v[8]);
+            f3 N = tvec(I16, normalize(cross(d2 - d0, d1 - d0)));      // Primitive.h:308-310
+            s0 = make_float4(N.x, N.y, N.z, ibits(p.material));
+        } else if (p.type == RT_SPHERE) {
+            float T[16];
+            translate_matrix(p.v[0], p.v[1], p.v[2], T);
+            f3 c = tpos(T, mk(0, 0, 0));
+            s0 = make_float4(c.x, c.y, c.z, ibits(p.material));
+            s1.y = 1.0f / p.v[3];                                      // data[0].z
+        } else {
+            s0 = make_float4(p.v[0], p.v[1], p.v[2], ibits(p.material));
+        }
+        shade[2 * id] = s0;
+        shade[2 * id + 1] = s1;
+    }
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t id = s->bvh.indices[k];
+        const rt_prim &p = d->prims[id];
+        float4 *q = &prims[3 * (size_t)k];
+        if (p.type == RT_TRIANGLE) {
+            f3 A = tpos(I16, mk(p.v[0], p.v[1], p.v[2]));                 // Intersect, Primitive.h:249-254
+            f3 B = tpos(I16, mk(p.v[3], p.v[4], p.v[5]));
+            f3 C = tpos(I16, mk(p.v[6], p.v[7], p.v[8]));
+            f3 AB = B - A, AC = C - A;
+            q[0] = make_float4(A.x, A.y, A.z, ibits((int)id));
+            q[1] = make_float4(AB.x, AB.y, AB.z, ubits(T_TRI));
+            q[2] = make_float4(AC.x, AC.y, AC.z, 0.0f);
+        } else if (p.type == RT_SPHERE) {
+            float T[16];
+            translate_matrix(p.v[0], p.v[1], p.v[2], T);
+            f3 c = tpos(T, mk(0, 0, 0));
+            float r = p.v[3];
+            q[0] = make_float4(c.x, c.y, c.z, ibits((int)id));
+            q[1] = make_float4(r * r, 0.0f, 0.0f, ubits(T_SPH)); // data[0].y
+            q[2] = make_float4(0, 0, 0, 0);
+        } else {
+            q[0] = make_float4(p.v[0], p.v[1], p.v[2], ibits((int)id));
+            q[1] = make_float4(p.v[3], 0.0f, 0.0f, ubits(T_PLANE));
+            q[2] = make_float4(0, 0, 0, 0);
+        }
+    }
+    // ---- materials
+    std::vector<DevMaterial> mats(d->num_materials);
+    for (uint32_t i = 0; i < d->num_materials; ++i) {
+        const rt_material &m = d->materials[i];
+        DevMaterial &o = mats[i];
+        std::memset(&o, 0, sizeof(o));
+        o.kind = m.kind;
+        if (m.kind < RT_DIFFUSE || m.kind > RT_LIGHT) { delete s; return fail(RT_ERR_INVALID, "unknown material kind"); }
+        for (int c = 0; c < 3; ++c) { o.c0[c] = m.color[c]; o.c1[c] = m.color2[c]; }
+        o.ior = m.ior;
+        if (m.kind == RT_CHECKERBOARD) {   // Checkerboard.h:6-14
+            if (m.diffuse < 0.0f) { o.diffuse = 1.0f; o.specular = 0.0f; }
+            else { o.diffuse = tmax(0.0f, tmin(m.diffuse, 1.0f)); o.specular = 1.0f - o.diffuse; }
+        }
+        o.flag = material_flag(m, o.diffuse, o.specular);
+    }
+    // ---- sky
+    std::vector<uint32_t> sky;
+    uint32_t sw = 1024, sh = 512;
+    if (d->sky_pixels) {
+        sw = d->sky_width; sh = d->sky_height;
+        sky.assign(d->sky_pixels, d->sky_pixels + (size_t)sw * sh);
+    } else {
+        sky.assign((size_t)sw * sh, 0x406080u);
+    }
+    bool sky_const = std::all_of(sky.begin(), sky.end(), [&](uint32_t v) { return v == sky[0]; });
+
+    rc = RT_OK;
+    if (rc == RT_OK) rc = upload(&s->d_nodes, nodes);
+    if (rc == RT_OK) rc = upload(&s->d_prims, prims);
+    if (rc == RT_OK) rc = upload(&s->d_shade, shade);
+    if (rc == RT_OK) rc = upload(&s->d_mats, mats);
+    if (rc == RT_OK) rc = upload(&s->d_sky, sky);
+    if (rc == RT_OK && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
+        rc = fail(RT_ERR_HIP, "hipStreamCreate failed");
+    if (rc != RT_OK) { free_scene(s); return rc; }
+
+    SceneView &v = s->view;
+    v.nodes = (const float4 *)s->d_nodes;
+    v.prims = (const float4 *)s->d_prims;
+    v.shade = (const float4 *)s->d_shade;
+    v.mats = (const DevMaterial *)s->d_mats;
+    v.sky = (const uint32_t *)s->d_sky;
+    v.sky_w = sw; v.sky_h = sh;
+    v.sky_const = sky_const ? 1 : 0;
+    {
+        uint32_t p = sky[0];
+        f3 c = mk((float)((p >> 16) & 255), (float)((p >> 8) & 255), (float)(p & 255)) * kSKY;
+        v.sky_rgb[0] = c.x; v.sky_rgb[1] = c.y; v.sky_rgb[2] = c.z;
+    }
+    const rt_prim &L = d->prims[0];
+    float T[16];
+    translate_matrix(L.v[0], L.v[1], L.v[2], T);
+    std::memcpy(v.light_M, T, sizeof(v.light_M));
+    f3 lc = tpos(T, mk(0, 0, 0));
+    v.light_c[0] = lc.x; v.light_c[1] = lc.y; v.light_c[2] = lc.z;
+    v.light_r = L.v[3];
+    v.light_r2 = L.v[3] * L.v[3];
+    v.light_invr = 1.0f / L.v[3];
+    v.light_mat = L.material;
+    const Node &root = s->bvh.nodes[0];
+    v.root_word = (root.leftFirst << 8) | root.count;
+    *out = s;
+    return RT_OK;
+}
+
+size_t stack_bytes(const rt_scene *s) { return (size_t)s->stack_depth * 256u * sizeof(uint32_t); }
+
+int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
+                  uint32_t *out, int packed, void *stream) {
+    if (!r || !cam || !p || !out) return fail(RT_ERR_INVALID, "rt_render: null argument");
+    if (p->width != r->W || p->height != r->H)
+        return fail(RT_ERR_INVALID, "frame size differs from the renderer's accumulator");
+    if (p->spp == 0) return fail(RT_ERR_INVALID, "spp must be >= 1");
+    if (p->mode != RT_MODE_PATH) return fail(RT_ERR_UNSUPPORTED, "only the path tracer (RT_MODE_PATH) is on the GPU path");
+    if (nshards == 0 || shard >= nshards) return fail(RT_ERR_INVALID, "bad shard index");
+    rt_scene *s = r->scene;
+    HIP_TRY(hipSetDevice(s->device));
+    FrameArgs F{};
+    for (int i = 0; i < 3; ++i) {
+        F.cam_pos[i] = cam->pos[i]; F.cam_tl[i] = cam->top_left[i];
+        F.cam_tr[i] = cam->top_right[i]; F.cam_bl[i] = cam->bottom_left[i];
+    }
+    F.lens = cam->lens_radius;
+    F.rw = 1.0f / (float)r->W;   // Camera::rWidth / rHeight (camera.h:98-99)
+    F.rh = 1.0f / (float)r->H;
+    F.W = r->W; F.H = r->H; F.spp = p->spp; F.depth = p->depth; F.frame = p->frame; F.reset = p->reset ? 1 : 0;
+    const uint32_t tiles_x = (r->W + 7) / 8, tiles_y = (r->H + 7) / 8, ntiles = tiles_x * tiles_y;
+    F.shard = shard; F.nshards = nshards; F.tiles_x = tiles_x;
+    F.ntiles_local = shard < ntiles ? (ntiles - shard + nshards - 1) / nshards : 0;
+    F.packed_out = packed;
+    F.acc = r->d_acc;
+    F.out = out;
+    F.counters = r->d_counters;
+    if (F.ntiles_local == 0) return RT_OK;
+    hipStream_t st = stream ? (hipStream_t)stream : r->stream;
+    dim3 grid((F.ntiles_local + 3) / 4), block(256);
+    const size_t lds = stack_bytes(s);
+    const uint32_t depth = p->depth;
+    if (depth <= 1) hipLaunchKernelGGL(k_render<1>, grid, block, lds, st, s->view, F);
+    else if (depth <= 4) hipLaunchKernelGGL(k_render<4>, grid, block, lds, st, s->view, F);
+    else if (depth <= 10) hipLaunchKernelGGL(k_render<10>, grid, block, lds, st, s->view, F);
+    else if (depth <= 32) hipLaunchKernelGGL(k_render<32>, grid, block, lds, st, s->view, F);
+    else return fail(RT_ERR_UNSUPPORTED, "Trace depth above 32");
+    HIP_TRY(hipGetLastError());
+    // pixels covered by this launch (primary rays per sample)
+    uint64_t px = (uint64_t)F.ntiles_local * 64u;
+    if ((r->W & 7u) || (r->H & 7u)) {
+        px = 0;
+        for (uint32_t t = shard; t < ntiles; t += nshards) {
+            uint32_t tx = t % tiles_x, ty = t / tiles_x;
+            px += (uint64_t)std::min(8u, r->W - tx * 8) * std::min(8u, r->H - ty * 8);
+        }
+    }
+    (void)tiles_y;
+    r->primary += px * p->spp;
+    r->frames += 1;
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_device_count(int *count) {
+    if (!count) return fail(RT_ERR_INVALID, "null count");
+    *count = 0;
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) return fail(RT_ERR_NO_DEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    *count = c;
+    return RT_OK;
+}
+
+int rt_scene_create(const rt_scene_desc *desc, rt_scene **out) {
+    try {
+        return scene_create(desc, out);
+    } catch (const std::exception &e) {
+        return fail(RT_ERR_INVALID, std::string("rt_scene_create: ") + e.what());
+    }
+}
+
+int rt_scene_create_recipe(const char *name, const char *mesh_dir, int32_t device, rt_scene **out) {
+    if (!name || !mesh_dir || !out) return fail(RT_ERR_INVALID, "rt_scene_create_recipe: null argument");
+    try {
+        SceneSource src;
+        int rc = recipe_source(name, mesh_dir, src);
+        if (rc != RT_OK) return rc;
+        rt_scene_desc d{};
+        d.prims = src.prims.data();
+        d.num_prims = (uint32_t)src.prims.size();
+        d.materials = src.materials.data();
+        d.num_materials = (uint32_t)src.materials.size();
+        d.device = device;
+        return scene_create(&d, out);
+    } catch (const std::exception &e) {
+        return fail(RT_ERR_INVALID, std::string("rt_scene_create_recipe: ") + e.what());
+    }
+}
+
+int rt_scene_destroy(rt_scene *s) {
+    free_scene(s);
+    return RT_OK;
+}
+
+int rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
+    if (!s || !info) return fail(RT_ERR_INVALID, "null argument");
+    info->num_prims = s->num_prims;
+    info->nodes_used = s->bvh.nodes_used;
+    info->depth = s->bvh.depth;
+    info->max_leaf = s->bvh.max_leaf;
+    return RT_OK;
+}
+
+int rt_scene_copy_bvh(const rt_scene *s, void *nodes, uint32_t *indices) {
+    if (!s || !nodes || !indices) return fail(RT_ERR_INVALID, "null argument");
+    std::memcpy(nodes, s->bvh.nodes.data(), sizeof(Node) * s->bvh.nodes_used);
+    std::memcpy(indices, s->bvh.indices.data(), sizeof(uint32_t) * s->num_prims);
+    return RT_OK;
+}
+
+int rt_intersect(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t n, void *stream) {
+    if (!s || (n && (!rays || !hits))) return fail(RT_ERR_INVALID, "rt_intersect: null argument");
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    hipLaunchKernelGGL(k_intersect, dim3((n + 255) / 256), dim3(256), stack_bytes(s), st, s->view, rays, hits, n);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+int rt_occluded(rt_scene *s, const rt_ray *rays, uint8_t *out, uint32_t n, void *stream) {
+    if (!s || (n && (!rays || !out))) return fail(RT_ERR_INVALID, "rt_occluded: null argument");
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    hipLaunchKernelGGL(k_occluded, dim3((n + 255) / 256), dim3(256), stack_bytes(s), st, s->view, rays, out, n);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+static int staged_call(rt_scene *s, const rt_ray *rays, void *out, size_t out_elem, uint32_t n, bool occl) {
+    if (!s || (n && (!rays || !out))) return fail(RT_ERR_INVALID, "null argument");
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    size_t need = (size_t)n * (sizeof(rt_ray) + out_elem) + 256;
+    if (need > s->scratch_bytes) {
+        if (s->d_scratch) HIP_TRY(hipFree(s->d_scratch));
+        s->d_scratch = nullptr;
+        s->scratch_bytes = 0;
+        HIP_TRY(hipMalloc(&s->d_scratch, need));
+        s->scratch_bytes = need;
+    }
+    rt_ray *d_rays = (rt_ray *)s->d_scratch;
+    char *d_out = (char *)s->d_scratch + (((size_t)n * sizeof(rt_ray) + 255) & ~(size_t)255);
+    HIP_TRY(hipMemcpyAsync(d_rays, rays, sizeof(rt_ray) * n, hipMemcpyHostToDevice, s->stream));
+    int rc = occl ? rt_occluded(s, d_rays, (uint8_t *)d_out, n, s->stream) : rt_intersect(s, d_rays, (rt_hit *)d_out, n, s->stream);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(out, d_out, out_elem * n, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return RT_OK;
+}
+
+int rt_intersect_host(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t n) {
+    return staged_call(s, rays, hits, sizeof(rt_hit), n, false);
+}
+int rt_occluded_host(rt_scene *s, const rt_ray *rays, uint8_t *out, uint32_t n) {
+    return staged_call(s, rays, out, 1, n, true);
+}
+
+int rt_renderer_create(rt_scene *s, uint32_t W, uint32_t H, rt_renderer **out) {
+    if (!s || !out || !W || !H) return fail(RT_ERR_INVALID, "rt_renderer_create: bad argument");
+    if ((uint64_t)W * H >= (1ull << 31)) return fail(RT_ERR_UNSUPPORTED, "frame too large");
+    HIP_TRY(hipSetDevice(s->device));
+    rt_renderer *r = new rt_renderer();
+    r->scene = s;
+    r->W = W; r->H = H;
+    hipError_t e = hipMalloc(&r->d_acc, sizeof(float4) * (size_t)W * H);   // Renderer::Init, renderer.cpp:6-12
+    if (e == hipSuccess) e = hipMemset(r->d_acc, 0, sizeof(float4) * (size_t)W * H);
+    if (e == hipSuccess) e = hipMalloc(&r->d_counters, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(r->d_counters, 0, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        if (r->d_acc) (void)hipFree(r->d_acc);
+        if (r->d_counters) (void)hipFree(r->d_counters);
+        delete r;
+        return fail(RT_ERR_HIP, std::string("rt_renderer_create: ") + hipGetErrorString(e));
+    }
+    *out = r;
+    return RT_OK;
+}
+
+int rt_renderer_destroy(rt_renderer *r) {
+    if (!r) return RT_OK;
+    (void)hipSetDevice(r->scene->device);
+    (void)hipStreamSynchronize(r->stream);
+    (void)hipFree(r->d_acc);
+    (void)hipFree(r->d_counters);
+    if (r->d_rgb) (void)hipFree(r->d_rgb);
+    (void)hipStreamDestroy(r->stream);
+    delete r;
+    return RT_OK;
+}
+
+int rt_render_frame(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t *rgb8, void *stream) {
+    return launch_render(r, cam, p, 0, 1, rgb8, 0, stream);
+}
+
+int rt_render_frame_host(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t *rgb8) {
+    if (!r || !rgb8) return fail(RT_ERR_INVALID, "rt_render_frame_host: null argument");
+    HIP_TRY(hipSetDevice(r->scene->device));
+    if (!r->d_rgb) HIP_TRY(hipMalloc(&r->d_rgb, sizeof(uint32_t) * (size_t)r->W * r->H));
+    int rc = launch_render(r, cam, p, 0, 1, r->d_rgb, 0, r->stream);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(rgb8, r->d_rgb, sizeof(uint32_t) * (size_t)r->W * r->H, hipMemcpyDeviceToHost, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    return RT_OK;
+}
+
+int rt_shard_capacity(uint32_t W, uint32_t H, uint32_t nshards, uint32_t *pixels) {
+    if (!pixels || !nshards || !W || !H) return fail(RT_ERR_INVALID, "rt_shard_capacity: bad argument");
+    uint32_t ntiles = ((W + 7) / 8) * ((H + 7) / 8);
+    *pixels = ((ntiles + nshards - 1) / nshards) * 64u;
+    return RT_OK;
+}
+
+int rt_render_shard(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
+                    uint32_t *tiles, void *stream) {
+    return launch_render(r, cam, p, shard, nshards, tiles, 1, stream);
+}
+
+int rt_assemble_shards(rt_renderer *r, const uint32_t *gathered, uint32_t nshards, uint32_t *rgb8, void *stream) {
+    if (!r || !gathered || !rgb8 || !nshards) return fail(RT_ERR_INVALID, "rt_assemble_shards: bad argument");
+    HIP_TRY(hipSetDevice(r->scene->device));
+    uint32_t cap = 0;
+    rt_shard_capacity(r->W, r->H, nshards, &cap);
+    uint32_t tiles_x = (r->W + 7) / 8, ntiles = tiles_x * ((r->H + 7) / 8);
+    hipStream_t st = stream ? (hipStream_t)stream : r->stream;
+    hipLaunchKernelGGL(k_assemble, dim3((ntiles + 3) / 4), dim3(256), 0, st, gathered, cap, nshards, tiles_x, ntiles,
+                       r->W, r->H, rgb8);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+int rt_renderer_counters(rt_renderer *r, rt_counters *out) {
+    if (!r || !out) return fail(RT_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(r->scene->device));
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long c[4];
+    HIP_TRY(hipMemcpy(c, r->d_counters, sizeof(c), hipMemcpyDeviceToHost));
+    out->primary = r->primary;
+    out->shadow = c[0];
+    out->bounce = c[1];
+    out->frames = r->frames;
+    return RT_OK;
+}
+
+int rt_renderer_read_accumulator(rt_renderer *r, float *host) {
+    if (!r || !host) return fail(RT_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(r->scene->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(host, r->d_acc, sizeof(float4) * (size_t)r->W * r->H, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_renderer_stream(rt_renderer *r, void **stream) {
+    if (!r || !stream) return fail(RT_ERR_INVALID, "null argument");
+    *stream = (void *)r->stream;
+    return RT_OK;
+}
+
+int rt_synchronize(rt_renderer *r) {
+    if (!r) return fail(RT_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(r->scene->device));
+    HIP_TRY(hipDeviceSynchronize());
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,606 @@
+// rt_host.cpp -- host-side scene preparation for the MI355X ray-tracing path.
+//
+// Everything here is a prerequisite of the GPU path, executed once per scene:
+//   * OBJ reading with tinyobj's exact number parsing and quad split, so vertex bits
+//     and primitive ids equal the reference's (Scene::LoadModel, template/scene.h:156-201);
+//   * mat4 construction / products (template/precomp.h:1007-1039, template.cpp:779-792);
+//   * the plain binned-SAH BVH (template/scene.h:845-976), built with an explicit work
+//     stack and precomputed per-primitive bounds, producing the identical node array;
+//   * the SURVEY.md 8(d) benchmark scenes.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "rt_internal.h"
+
+namespace rt {
+
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+int fail(int code, const std::string &msg) { g_err = msg; return code; }
+
+// ------------------------------------------------------------------ mat4
+static void identity(float M[16]) { std::memset(M, 0, 64); M[0] = M[5] = M[10] = M[15] = 1.0f; }
+void translate_matrix(float x, float y, float z, float M[16]) { identity(M); M[3] = x; M[7] = y; M[11] = z; }
+static void mat_mul(const float *a, const float *b, float *out) {
+    float r[16];
+    for (int i = 0; i < 16; i += 4)
+        for (int j = 0; j < 4; ++j)
+            r[i + j] = (a[i + 0] * b[j + 0]) + (a[i + 1] * b[j + 4]) + (a[i + 2] * b[j + 8]) + (a[i + 3] * b[j + 12]);
+    std::memcpy(out, r, 64);
+}
+static void mat_rotate(int axis, float a, float M[16]) {   // precomp.h:1007-1009
+    identity(M);
+    if (axis == 0) { M[5] = cosf(a); M[6] = -sinf(a); M[9] = sinf(a); M[10] = cosf(a); }
+    else if (axis == 1) { M[0] = cosf(a); M[2] = sinf(a); M[8] = -sinf(a); M[10] = cosf(a); }
+    else { M[0] = cosf(a); M[1] = -sinf(a); M[4] = sinf(a); M[5] = cosf(a); }
+}
+static const float kIdentity[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+
+// ------------------------------------------------------------------ OBJ (tinyobj restatement)
+namespace obj {
+inline bool digit(char c) { return (unsigned)(c - '0') < 10u; }
+
+// tryParseDouble, template/tiny_obj_loader.h:887-1016 -- the mantissa is accumulated in
+// double exactly as tinyobj does, so the float cast yields the reference's vertex bits.
+bool parse_double(const char *s, const char *end, double *out) {
+    if (s >= end) return false;
+    double mant = 0.0;
+    int exponent = 0, read = 0;
+    char sign = '+', esign = '+';
+    const char *c = s;
+    bool more = false, leading_dot = false;
+    if (*c == '+' || *c == '-') {
+        sign = *c++;
+        if (c != end && *c == '.') leading_dot = true;
+    } else if (*c == '.') {
+        leading_dot = true;
+    } else if (!digit(*c)) {
+        return false;
+    }
+    more = (c != end);
+    if (!leading_dot) {
+        while (more && digit(*c)) { mant *= 10; mant += static_cast<int>(*c - 0x30); ++c; ++read; more = (c != end); }
+        if (read == 0) return false;
+    }
+    if (more) {
+        bool exp_next = false;
+        if (*c == '.') {
+            ++c; read = 1; more = (c != end);
+            static const double lut[] = {1.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001};
+            while (more && digit(*c)) {
+                mant += static_cast<int>(*c - 0x30) * (read < 8 ? lut[read] : std::pow(10.0, -read));
+                ++read; ++c; more = (c != end);
+            }
+            exp_next = more;
+        } else if (*c == 'e' || *c == 'E') {
+            exp_next = true;
+        }
+        if (exp_next && (*c == 'e' || *c == 'E')) {
+            ++c; more = (c != end);
+            if (more && (*c == '+' || *c == '-')) esign = *c++;
+            else if (!digit(*c)) return false;
+            read = 0; more = (c != end);
+            while (more && digit(*c)) {
+                if (exponent > 2147483647 / 10) return false;
+                exponent = exponent * 10 + static_cast<int>(*c - 0x30);
+                ++c; ++read; more = (c != end);
+            }
+            exponent *= (esign == '+' ? 1 : -1);
+            if (read == 0) return false;
+        }
+    }
+    *out = (sign == '+' ? 1 : -1) * (exponent ? std::ldexp(mant * std::pow(5.0, exponent), exponent) : mant);
+    return true;
+}
+
+float real_token(const char *&tok) {   // parseReal, 1019-1027
+    tok += std::strspn(tok, " \t");
+    const char *end = tok + std::strcspn(tok, " \t\r");
+    double v = 0.0;
+    parse_double(tok, end, &v);
+    tok = end;
+    return static_cast<float>(v);
+}
+
+bool vertex_index(int idx, int n, int &out) {   // fixIndex, position slot (allow_zero = false)
+    if (idx > 0) { out = idx - 1; return true; }
+    if (idx == 0) return false;
+    out = n + idx;
+    return out >= 0;
+}
+
+struct Reader {
+    std::vector<float> v;
+    std::vector<int32_t> f;
+
+    void face(const std::vector<int> &ids) {
+        size_t n = ids.size();
+        if (n < 3) return;                                   // degenerate face
+        if (n == 3) { f.insert(f.end(), ids.begin(), ids.end()); return; }
+        if (n == 4) {                                        // 1484-1580: split along the shorter diagonal
+            for (int id : ids)
+                if (3 * (size_t)id + 2 >= v.size()) return;  // invalid quad is skipped, 1496-1503
+            const float *p0 = &v[3 * ids[0]], *p1 = &v[3 * ids[1]], *p2 = &v[3 * ids[2]], *p3 = &v[3 * ids[3]];
+            float ax = p2[0] - p0[0], ay = p2[1] - p0[1], az = p2[2] - p0[2];
+            float bx = p3[0] - p1[0], by = p3[1] - p1[1], bz = p3[2] - p1[2];
+            float s02 = ax * ax + ay * ay + az * az, s13 = bx * bx + by * by + bz * bz;
+            const int q[2][6] = {{0, 1, 2, 0, 2, 3}, {0, 1, 3, 1, 2, 3}};
+            const int *sel = q[s02 < s13 ? 0 : 1];
+            for (int k = 0; k < 6; ++k) f.push_back(ids[sel[k]]);
+            return;
+        }
+        for (size_t k = 1; k + 1 < n; ++k) { f.push_back(ids[0]); f.push_back(ids[k]); f.push_back(ids[k + 1]); }
+    }
+
+    int line(const std::string &ln) {
+        const char *t = ln.c_str();
+        t += std::strspn(t, " \t");
+        if (!*t || *t == '#') return 0;
+        if (t[0] == 'v' && (t[1] == ' ' || t[1] == '\t')) {
+            t += 2;
+            for (int k = 0; k < 3; ++k) v.push_back(real_token(t));
+            return 0;
+        }
+        if (t[0] == 'f' && (t[1] == ' ' || t[1] == '\t')) {
+            t += 2;
+            t += std::strspn(t, " \t");
+            std::vector<int> ids;
+            while (*t && *t != '\r' && *t != '\n') {
+                int vi;
+                if (!vertex_index(std::atoi(t), static_cast<int>(v.size() / 3), vi)) return -1;
+                ids.push_back(vi);
+                t += std::strcspn(t, " \t\r");
+                t += std::strspn(t, " \t\r");
+            }
+            face(ids);
+        }
+        return 0;
+    }
+};
+}  // namespace obj
+
+// ------------------------------------------------------------------ primitive geometry
+void prim_geometry(const rt_prim &p, PrimGeom &g) {
+    if (p.type == RT_SPHERE) {
+        float T[16];
+        translate_matrix(p.v[0], p.v[1], p.v[2], T);
+        f3 c = tpos(T, mk(0, 0, 0));
+        float r = p.v[3];
+        g.centroid = c;                       // centroid float3(0) through Transform
+        g.bmin = c - mk(r, r, r);
+        g.bmax = c + mk(r, r, r);
+    } else if (p.type == RT_PLANE) {
+        f3 n = mk(p.v[0], p.v[1], p.v[2]);
+        g.centroid = tpos(kIdentity, (-n) * p.v[3]);
+        g.bmin = mk(-1e30f, -1e30f, -1e30f);
+        g.bmax = mk(1e30f, 1e30f, 1e30f);
+    } else {
+        f3 d0 = mk(p.v[0], p.v[1], p.v[2]), d1 = mk(p.v[3], p.v[4], p.v[5]), d2 = mk(p.v[6], p.v[7], p.v[8]);
+        f3 A = tpos(kIdentity, d0), B = tpos(kIdentity, d1), C = tpos(kIdentity, d2);
+        g.centroid = tpos(kIdentity, ((d0 + d1) + d2) / 3.0f);
+        g.bmin = fmin3(A, fmin3(B, C));
+        g.bmax = fmax3(A, fmax3(B, C));
+    }
+}
+
+// ------------------------------------------------------------------ BVH
+namespace {
+struct Box { f3 mn, mx; };
+inline Box empty_box() { return {mk(1e34f, 1e34f, 1e34f), mk(-1e34f, -1e34f, -1e34f)}; }   // aabb default
+inline void grow(Box &b, f3 p) { b.mn = fmin3(b.mn, p); b.mx = fmax3(b.mx, p); }           // _mm_min/max_ps
+inline void grow(Box &b, const Box &o) { b.mn = fmin3(b.mn, o.mn); b.mx = fmax3(b.mx, o.mx); }
+inline float area(const Box &b) {                                                      // aabb::Area
+    float e0 = b.mx.x - b.mn.x, e1 = b.mx.y - b.mn.y, e2 = b.mx.z - b.mn.z;
+    return smax(0.0f, e0 * e1 + e0 * e2 + e1 * e2);
+}
+
+class Builder {
+  public:
+    Builder(const std::vector<PrimGeom> &g, Bvh &b) : geo_(g), bvh_(b) {}
+
+    void run(uint32_t n) {
+        bvh_.indices.resize(n);
+        for (uint32_t i = 0; i < n; ++i) bvh_.indices[i] = i;
+        bvh_.nodes.assign(2 * (size_t)n + 2, Node{});
+        bvh_.nodes[0].leftFirst = 0;
+        bvh_.nodes[0].count = n;
+        bvh_.nodes_used = 2;   // node 1 skipped for 64-byte child pairs (scene.h:849)
+        refit(0);
+        // depth-first, left before right: the same allocation order as the recursion
+        std::vector<uint32_t> work{0};
+        while (!work.empty()) {
+            uint32_t ni = work.back();
+            work.pop_back();
+            uint32_t l;
+            if (split(ni, l)) { work.push_back(l + 1); work.push_back(l); }
+        }
+        bvh_.depth = depth(0);
+        bvh_.max_leaf = 0;
+        for (uint32_t i = 0; i < bvh_.nodes_used; ++i)
+            if (i != 1 && bvh_.nodes[i].count > bvh_.max_leaf) bvh_.max_leaf = bvh_.nodes[i].count;
+    }
+
+  private:
+    const std::vector<PrimGeom> &geo_;
+    Bvh &bvh_;
+
+    void refit(uint32_t ni) {   // UpdateNodeBounds
+        Node &n = bvh_.nodes[ni];
+        f3 mn = mk(1e30f, 1e30f, 1e30f), mx = mk(-1e30f, -1e30f, -1e30f);
+        for (uint32_t i = 0; i < n.count; ++i) {
+            const PrimGeom &g = geo_[bvh_.indices[n.leftFirst + i]];
+            mn = fmin3(mn, g.bmin);
+            mx = fmax3(mx, g.bmax);
+        }
+        n.mn[0] = mn.x; n.mn[1] = mn.y; n.mn[2] = mn.z;
+        n.mx[0] = mx.x; n.mx[1] = mx.y; n.mx[2] = mx.z;
+    }
+
+    float best_plane(const Node &n, int &axis, float &pos) const {   // FindBestSplitPlane
+        float best = 1e30f;
+        const uint32_t *ix = bvh_.indices.data() + n.leftFirst;
+        for (int a = 0; a < 3; ++a) {
+            float lo = 1e30f, hi = -1e30f;
+            for (uint32_t i = 0; i < n.count; ++i) {
+                float c = comp(geo_[ix[i]].centroid, a);
+                lo = smin(lo, c);
+                hi = smax(hi, c);
+            }
+            if (lo == hi) continue;
+            Box bins[32];
+            int cnt[32] = {0};
+            for (auto &b : bins) b = empty_box();
+            float scale = 32 / (hi - lo);
+            for (uint32_t i = 0; i < n.count; ++i) {
+                const PrimGeom &g = geo_[ix[i]];
+                int b = static_cast<int>((comp(g.centroid, a) - lo) * scale);
+                b = b < 31 ? b : 31;
+                cnt[b]++;
+                grow(bins[b], g.bmin);
+                grow(bins[b], g.bmax);
+            }
+            float la[31], ra[31];
+            int lc[31], rc[31];
+            Box L = empty_box(), R = empty_box();
+            int ls = 0, rs = 0;
+            for (int i = 0; i < 31; ++i) {
+                ls += cnt[i]; lc[i] = ls; grow(L, bins[i]); la[i] = area(L);
+                rs += cnt[31 - i]; rc[30 - i] = rs; grow(R, bins[31 - i]); ra[30 - i] = area(R);
+            }
+            float step = (hi - lo) / 32;
+            for (int i = 0; i < 31; ++i) {
+                float cost = (float)lc[i] * la[i] + (float)rc[i] * ra[i];
+                if (cost < best) { axis = a; pos = lo + step * (float)(i + 1); best = cost; }
+            }
+        }
+        return best;
+    }
+
+    bool split(uint32_t ni, uint32_t &left) {   // Subdivide, minus the recursion
+        Node n = bvh_.nodes[ni];
+        int axis = 0;
+        float pos = 0.0f;
+        float cost = best_plane(n, axis, pos);
+        float ex = n.mx[0] - n.mn[0], ey = n.mx[1] - n.mn[1], ez = n.mx[2] - n.mn[2];
+        if (cost >= (float)n.count * (ex * ey + ey * ez + ez * ex)) return false;
+        int i = (int)n.leftFirst, j = i + (int)n.count - 1;
+        uint32_t *ix = bvh_.indices.data();
+        while (i <= j) {
+            if (comp(geo_[ix[i]].centroid, axis) < pos) ++i;
+            else std::swap(ix[i], ix[j--]);
+        }
+        int lcount = i - (int)n.leftFirst;
+        if (lcount == 0 || lcount == (int)n.count) return false;
+        left = bvh_.nodes_used;
+        bvh_.nodes_used += 2;
+        Node &l = bvh_.nodes[left], &r = bvh_.nodes[left + 1];
+        l.leftFirst = n.leftFirst; l.count = (uint32_t)lcount;
+        r.leftFirst = (uint32_t)i; r.count = n.count - (uint32_t)lcount;
+        bvh_.nodes[ni].leftFirst = left;
+        bvh_.nodes[ni].count = 0;
+        refit(left);
+        refit(left + 1);
+        return true;
+    }
+
+    uint32_t depth(uint32_t ni) const {   // maxDepthBVH, iterative
+        std::vector<std::pair<uint32_t, uint32_t>> st{{ni, 0}};
+        uint32_t best = 0;
+        while (!st.empty()) {
+            auto [k, d] = st.back();
+            st.pop_back();
+            const Node &n = bvh_.nodes[k];
+            if (n.count > 0) { best = std::max(best, k == 0 ? 1u : d); continue; }
+            st.push_back({n.leftFirst, d + 1});
+            st.push_back({n.leftFirst + 1, d + 1});
+        }
+        return best;
+    }
+};
+}  // namespace
+
+int build_bvh(const rt_prim *prims, uint32_t n, Bvh &out) {
+    if (n == 0) return fail(RT_ERR_INVALID, "scene has no primitives");
+    std::vector<PrimGeom> geo(n);
+    for (uint32_t i = 0; i < n; ++i) prim_geometry(prims[i], geo[i]);
+    Builder(geo, out).run(n);
+    return RT_OK;
+}
+
+// ------------------------------------------------------------------ mesh container
+static int mesh_read(const std::string &path, std::vector<float> &V, std::vector<int32_t> &F) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) return fail(RT_ERR_IO, "cannot open " + path);
+    char magic[8];
+    uint32_t h[2];
+    in.read(magic, 8);
+    in.read(reinterpret_cast<char *>(h), 8);
+    if (!in || std::memcmp(magic, "RTMESH1", 8) != 0) return fail(RT_ERR_IO, "not an RTMESH1 file: " + path);
+    V.resize(3 * (size_t)h[0]);
+    F.resize(3 * (size_t)h[1]);
+    in.read(reinterpret_cast<char *>(V.data()), 4 * V.size());
+    in.read(reinterpret_cast<char *>(F.data()), 4 * F.size());
+    if (!in) return fail(RT_ERR_IO, "truncated RTMESH1 file: " + path);
+    for (int32_t f : F)
+        if (f < 0 || (uint32_t)f >= h[0]) return fail(RT_ERR_IO, "face index out of range in " + path);
+    return RT_OK;
+}
+
+static void append_mesh(const std::vector<float> &V, const std::vector<int32_t> &F, const float M[16], int32_t mat,
+                        std::vector<rt_prim> &out) {
+    size_t nt = F.size() / 3;
+    size_t base = out.size();
+    out.resize(base + nt);
+    for (size_t f = 0; f < nt; ++f) {
+        rt_prim &p = out[base + f];
+        p.type = RT_TRIANGLE;
+        p.material = mat;
+        for (int k = 0; k < 3; ++k) {
+            const float *q = &V[3 * (size_t)F[3 * f + k]];
+            f3 w = tpos(M, mk(q[0], q[1], q[2]));   // TransformPosition(float3(vx,vy,vz), transform)
+            p.v[3 * k] = w.x; p.v[3 * k + 1] = w.y; p.v[3 * k + 2] = w.z;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ SURVEY 8(d) scenes
+int recipe_source(const std::string &name, const std::string &dir, SceneSource &out) {
+    out.prims.clear();
+    out.materials.clear();
+    auto material = [&](int32_t kind, f3 c, f3 c2 = mk(0, 0, 0), float ior = 0, float diffuse = -1.0f) {
+        rt_material m{};
+        m.kind = kind;
+        m.color[0] = c.x; m.color[1] = c.y; m.color[2] = c.z;
+        m.color2[0] = c2.x; m.color2[1] = c2.y; m.color2[2] = c2.z;
+        m.ior = ior;
+        m.diffuse = diffuse;
+        out.materials.push_back(m);
+        return (int32_t)out.materials.size() - 1;
+    };
+    auto sphere = [&](f3 c, float r, int32_t mat) {
+        rt_prim p{};
+        p.type = RT_SPHERE; p.material = mat;
+        p.v[0] = c.x; p.v[1] = c.y; p.v[2] = c.z; p.v[3] = r;
+        out.prims.push_back(p);
+    };
+    auto tri = [&](f3 a, f3 b, f3 c, int32_t mat) {
+        rt_prim p{};
+        p.type = RT_TRIANGLE; p.material = mat;
+        f3 v[3] = {a, b, c};
+        for (int k = 0; k < 3; ++k) { p.v[3 * k] = v[k].x; p.v[3 * k + 1] = v[k].y; p.v[3 * k + 2] = v[k].z; }
+        out.prims.push_back(p);
+    };
+    auto mesh = [&](const char *file, const float M[16], int32_t mat) {
+        std::vector<float> V;
+        std::vector<int32_t> F;
+        int rc = mesh_read(dir + "/" + file + ".rtmesh", V, F);
+        if (rc == RT_OK) append_mesh(V, F, M, mat, out.prims);
+        return rc;
+    };
+    auto floor2 = [&](int32_t mat) {   // the two checkerboard floor triangles of SURVEY 8(d)
+        const float y = -1.225f;
+        tri(mk(-20, y, -1), mk(20, y, -1), mk(20, y, 40), mat);
+        tri(mk(-20, y, -1), mk(20, y, 40), mk(-20, y, 40), mat);
+    };
+    auto chain = [](std::initializer_list<const float *> ms, float *M) {
+        auto it = ms.begin();
+        std::memcpy(M, *it, 64);
+        for (++it; it != ms.end(); ++it) mat_mul(M, *it, M);
+    };
+
+    int32_t lamp = material(RT_LIGHT, mk(24.0f, 24.0f, 22.0f));          // scene.h:55
+    int32_t white = material(RT_DIFFUSE, mk(0.95f, 0.95f, 0.95f));       // scene.h:46
+    int32_t green = material(RT_DIFFUSE, mk(0.05f, 0.95f, 0.05f));       // scene.h:44
+    int32_t check = material(RT_CHECKERBOARD, mk(0.1f, 0.1f, 0.1f), mk(0.9f, 0.9f, 0.9f));   // scene.h:50
+    bool high_light = (name == "teapot" || name == "mig16");
+    sphere(high_light ? mk(0.0f, 6.0f, 5.0f) : mk(0.0f, 4.0f, -2.0f), 0.5f, lamp);
+
+    float T[16], R[16], R2[16], R3[16], S[16], M[16];
+    int rc = RT_OK;
+    if (name == "teapotF" || name == "teapot") {
+        bool f = (name == "teapotF");
+        translate_matrix(0, 0, f ? 2.0f : 1.5f, T);
+        mat_rotate(1, 0.5f * kPI, R);
+        identity(S); S[0] = S[5] = S[10] = f ? 2.5f : 1.5f;
+        chain({T, R, S}, M);
+        rc = mesh("teapot", M, white);
+        if (f) floor2(check);
+    } else if (name == "mig16") {
+        for (int i = 0; i < 16 && rc == RT_OK; ++i) {
+            float x = (float)(i % 4) - 1.5f, y = (float)(i / 4) - 1.5f;
+            translate_matrix(x * 1.8f, y * 1.1f - 0.3f, 2.5f, T);
+            mat_rotate(0, 0.3f * kPI, R);
+            identity(S); S[0] = S[5] = S[10] = 0.01f;
+            chain({T, R, S}, M);
+            rc = mesh("mig29", M, green);
+        }
+    } else if (name == "cfg3") {
+        int32_t glass = material(RT_DIELECTRIC, mk(0.5f, 0.5f, 0.5f), mk(0, 0, 0), 1.52f);
+        int32_t mirror = material(RT_MIRROR, mk(0.9f, 0.75f, 0.0f));
+        translate_matrix(0, -1, 2, T);
+        identity(S); S[0] = S[5] = S[10] = 8.0f;
+        chain({T, S}, M);
+        rc = mesh("Shiba", M, glass);
+        if (rc == RT_OK) {   // glider transform, template/scene.h:88
+            translate_matrix(1.0f, 0.0f, 0.0f, T);
+            mat_rotate(2, -0.15f * kPI, R); mat_rotate(1, 0.05f * kPI, R2); mat_rotate(0, -0.55f * kPI, R3);
+            identity(S); S[0] = S[5] = S[10] = 0.025f;
+            chain({T, R, R2, R3, S}, M);
+            rc = mesh("glider", M, mirror);
+        }
+        floor2(check);
+    } else if (name == "cfg5") {
+        translate_matrix(0, -1.2f, 2.5f, T);
+        identity(S); S[0] = S[5] = S[10] = 12.0f;
+        chain({T, S}, M);
+        rc = mesh("Shiba", M, white);
+        floor2(check);
+    } else {
+        return fail(RT_ERR_INVALID, "unknown scene recipe '" + name + "'");
+    }
+    return rc;
+}
+
+}  // namespace rt
+
+using namespace rt;
+
+// ------------------------------------------------------------------ C-ABI: host-side entry points
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+const char *rt_last_error(void) { return g_err.c_str(); }
+void rt_free(void *p) { std::free(p); }
+
+int rt_obj_load(const char *path, float **verts, uint32_t *nv, int32_t **faces, uint32_t *nt) {
+    if (!path || !verts || !nv || !faces || !nt) return fail(RT_ERR_INVALID, "rt_obj_load: null argument");
+    std::ifstream in(path, std::ios::binary);
+    if (!in) return fail(RT_ERR_IO, std::string("cannot open ") + path);
+    obj::Reader rd;
+    std::string line;
+    size_t lineno = 0;
+    while (std::getline(in, line)) {   // '\n' lines; the trailing '\r' of CRLF is skipped by the tokenizer
+        ++lineno;
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        if (rd.line(line) != 0) return fail(RT_ERR_IO, "bad face at line " + std::to_string(lineno) + " of " + path);
+    }
+    *nv = (uint32_t)(rd.v.size() / 3);
+    *nt = (uint32_t)(rd.f.size() / 3);
+    *verts = static_cast<float *>(std::malloc(sizeof(float) * (rd.v.size() ? rd.v.size() : 1)));
+    *faces = static_cast<int32_t *>(std::malloc(sizeof(int32_t) * (rd.f.size() ? rd.f.size() : 1)));
+    std::memcpy(*verts, rd.v.data(), sizeof(float) * rd.v.size());
+    std::memcpy(*faces, rd.f.data(), sizeof(int32_t) * rd.f.size());
+    return RT_OK;
+}
+
+int rt_mesh_load(const char *path, float **verts, uint32_t *nv, int32_t **faces, uint32_t *nt) {
+    if (!path || !verts || !nv || !faces || !nt) return fail(RT_ERR_INVALID, "rt_mesh_load: null argument");
+    std::vector<float> V;
+    std::vector<int32_t> F;
+    int rc = mesh_read(path, V, F);
+    if (rc != RT_OK) return rc;
+    *nv = (uint32_t)(V.size() / 3);
+    *nt = (uint32_t)(F.size() / 3);
+    *verts = static_cast<float *>(std::malloc(sizeof(float) * (V.size() ? V.size() : 1)));
+    *faces = static_cast<int32_t *>(std::malloc(sizeof(int32_t) * (F.size() ? F.size() : 1)));
+    std::memcpy(*verts, V.data(), sizeof(float) * V.size());
+    std::memcpy(*faces, F.data(), sizeof(int32_t) * F.size());
+    return RT_OK;
+}
+
+int rt_mesh_save(const char *path, const float *verts, uint32_t nv, const int32_t *faces, uint32_t nt) {
+    if (!path || (nv && !verts) || (nt && !faces)) return fail(RT_ERR_INVALID, "rt_mesh_save: null argument");
+    std::ofstream out(path, std::ios::binary);
+    if (!out) return fail(RT_ERR_IO, std::string("cannot write ") + path);
+    uint32_t h[2] = {nv, nt};
+    out.write("RTMESH1", 8);
+    out.write(reinterpret_cast<const char *>(h), 8);
+    out.write(reinterpret_cast<const char *>(verts), 12 * (size_t)nv);
+    out.write(reinterpret_cast<const char *>(faces), 12 * (size_t)nt);
+    return out ? RT_OK : fail(RT_ERR_IO, std::string("short write to ") + path);
+}
+
+int rt_mat4_translate(float x, float y, float z, float out[16]) {
+    if (!out) return fail(RT_ERR_INVALID, "null matrix");
+    translate_matrix(x, y, z, out);
+    return RT_OK;
+}
+int rt_mat4_scale(float s, float out[16]) {
+    if (!out) return fail(RT_ERR_INVALID, "null matrix");
+    identity(out);
+    out[0] = out[5] = out[10] = s;
+    return RT_OK;
+}
+int rt_mat4_rotate(int axis, float angle, float out[16]) {
+    if (!out || axis < 0 || axis > 2) return fail(RT_ERR_INVALID, "rt_mat4_rotate: axis must be 0, 1 or 2");
+    mat_rotate(axis, angle, out);
+    return RT_OK;
+}
+int rt_mat4_mul(const float a[16], const float b[16], float out[16]) {
+    if (!a || !b || !out) return fail(RT_ERR_INVALID, "null matrix");
+    mat_mul(a, b, out);
+    return RT_OK;
+}
+
+int rt_mesh_to_prims(const float *verts, uint32_t nv, const int32_t *faces, uint32_t nt, const float M[16],
+                     int32_t material, rt_prim *out) {
+    if (!verts || !faces || !M || !out) return fail(RT_ERR_INVALID, "rt_mesh_to_prims: null argument");
+    for (uint32_t i = 0; i < 3 * nt; ++i)
+        if (faces[i] < 0 || (uint32_t)faces[i] >= nv) return fail(RT_ERR_INVALID, "face index out of range");
+    std::vector<float> V(verts, verts + 3 * (size_t)nv);
+    std::vector<int32_t> F(faces, faces + 3 * (size_t)nt);
+    std::vector<rt_prim> tmp;
+    append_mesh(V, F, M, material, tmp);
+    std::memcpy(out, tmp.data(), sizeof(rt_prim) * tmp.size());
+    return RT_OK;
+}
+
+int rt_recipe_describe(const char *name, const char *mesh_dir, rt_prim *prims, uint32_t *num_prims,
+                       rt_material *materials, uint32_t *num_materials) {
+    if (!name || !mesh_dir || !num_prims || !num_materials) return fail(RT_ERR_INVALID, "rt_recipe_describe: null argument");
+    SceneSource src;
+    int rc = recipe_source(name, mesh_dir, src);
+    if (rc != RT_OK) return rc;
+    if (prims) {
+        if (*num_prims < src.prims.size() || *num_materials < src.materials.size() || !materials)
+            return fail(RT_ERR_INVALID, "rt_recipe_describe: arrays too small");
+        std::memcpy(prims, src.prims.data(), sizeof(rt_prim) * src.prims.size());
+        std::memcpy(materials, src.materials.data(), sizeof(rt_material) * src.materials.size());
+    }
+    *num_prims = (uint32_t)src.prims.size();
+    *num_materials = (uint32_t)src.materials.size();
+    return RT_OK;
+}
+
+int rt_bvh_build_host(const rt_prim *prims, uint32_t n, void *nodes, uint32_t *indices, rt_scene_info *info) {
+    if (!prims || !nodes || !indices) return fail(RT_ERR_INVALID, "rt_bvh_build_host: null argument");
+    Bvh b;
+    int rc = build_bvh(prims, n, b);
+    if (rc != RT_OK) return rc;
+    std::memcpy(nodes, b.nodes.data(), sizeof(Node) * b.nodes.size());
+    std::memcpy(indices, b.indices.data(), sizeof(uint32_t) * n);
+    if (info) { info->num_prims = n; info->nodes_used = b.nodes_used; info->depth = b.depth; info->max_leaf = b.max_leaf; }
+    return RT_OK;
+}
+
+int rt_camera_default(uint32_t W, uint32_t H, rt_camera *c) {   // camera.h:28-41, 93-100
+    if (!c || !W || !H) return fail(RT_ERR_INVALID, "rt_camera_default: bad argument");
+    float aperture = (float)0.000005;
+    float lens = aperture / 2.0f, focus = 1.0f, fov = 1.0f;
+    float aspect = (float)W / (float)H;
+    f3 pos = mk(0, 0, -fov);
+    f3 tl = pos + focus * mk(-aspect, 1, fov), tr = pos + focus * mk(aspect, 1, fov), bl = pos + focus * mk(-aspect, -1, fov);
+    const f3 *src[4] = {&pos, &tl, &tr, &bl};
+    float *dst[4] = {c->pos, c->top_left, c->top_right, c->bottom_left};
+    for (int i = 0; i < 4; ++i) { dst[i][0] = src[i]->x; dst[i][1] = src[i]->y; dst[i][2] = src[i]->z; }
+    c->lens_radius = lens;
+    return RT_OK;
+}
+
+}  // extern "C"

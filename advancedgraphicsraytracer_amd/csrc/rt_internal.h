@@ -1,0 +1,43 @@
+// rt_internal.h -- host-side internals shared by rt_host.cpp and rt_device.hip.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "../../include/rt_amd.h"
+#include "rt_math.h"
+
+namespace rt {
+
+// thread-local error message for rt_last_error()
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+// 32-byte BVHNode (BVHNode.h:5-14): aabbMin, aabbMax, leftFirst, primitiveCount
+struct Node {
+    float mn[3], mx[3];
+    uint32_t leftFirst, count;
+};
+static_assert(sizeof(Node) == 32, "BVHNode layout");
+
+// Per-primitive geometry the builder and the uploader need, evaluated exactly as
+// Primitive::GetCentroid / GetAABBMin / GetAABBMax (Primitive.h:42-50, 319-388, 443-445).
+struct PrimGeom { f3 centroid, bmin, bmax; };
+void prim_geometry(const rt_prim &p, PrimGeom &g);
+void translate_matrix(float x, float y, float z, float M[16]);
+
+// Plain binned-SAH BVH (template/scene.h:845-976).  nodes sized 2N+2, indices N.
+struct Bvh {
+    std::vector<Node> nodes;
+    std::vector<uint32_t> indices;
+    uint32_t nodes_used = 0, depth = 0, max_leaf = 0;
+};
+int build_bvh(const rt_prim *prims, uint32_t n, Bvh &out);
+
+// SURVEY.md 8(d) scenes as descriptions
+struct SceneSource {
+    std::vector<rt_prim> prims;
+    std::vector<rt_material> materials;
+};
+int recipe_source(const std::string &name, const std::string &mesh_dir, SceneSource &out);
+
+}  // namespace rt

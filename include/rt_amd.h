@@ -1,0 +1,174 @@
+/*
+ * rt_amd.h -- C-ABI of the MI355X-native ray-tracing hot path (librtamd.so).
+ *
+ * Drop-in boundary for the reference's Renderer::Tick / Renderer::Trace /
+ * Scene::IntersectBVH / Scene::IsOccluded path (pmichels19/AdvancedGraphicsRayTracer).
+ * The reference has no FFI of its own: its "boundary" is the in-process C++ class
+ * surface cited on each entry point below.  A C++ host binds these functions
+ * directly (see include/rt_compat.hpp); Python binds them with ctypes
+ * (advancedgraphicsraytracer_amd/__init__.py).
+ *
+ * Conventions
+ *   - every entry point is extern "C", returns int status (RT_OK = 0, < 0 error),
+ *     and never throws; rt_last_error() returns a thread-local message;
+ *   - scene/renderer handles are opaque; the library owns all device buffers it
+ *     allocates; pointers named *_dev are caller-owned DEVICE memory, the rest are
+ *     caller-owned host memory;
+ *   - stream arguments are hipStream_t passed as void* (NULL = the library's stream
+ *     of that handle);
+ *   - primitive ids follow creation order exactly as the reference's
+ *     Primitive::objIdx (Primitive.h:37-38); the light is primitive 0 and must be a
+ *     sphere (Scene::GetRandomLight, template/scene.h:225-227).
+ * No CPU fallback exists: without a usable gfx950 device every compute entry
+ * point fails with RT_ERR_NO_DEVICE.
+ */
+#ifndef RT_AMD_H
+#define RT_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,    /* bad argument */
+    RT_ERR_NO_DEVICE = -2,  /* no HIP device / kernel image not loadable */
+    RT_ERR_HIP = -3,        /* HIP runtime error */
+    RT_ERR_IO = -4,         /* file not found / parse error */
+    RT_ERR_UNSUPPORTED = -5 /* scene outside the kernels' limits */
+};
+
+/* Primitive kinds, Primitive.h:8-14 (CUBE and QUAD are not on the hot path). */
+enum { RT_SPHERE = 0, RT_PLANE = 1, RT_TRIANGLE = 4 };
+/* Materials: Diffuse.h, Mirror.h, Dielectric.h, Checkerboard.h, Light.h. */
+enum { RT_DIFFUSE = 0, RT_MIRROR = 1, RT_DIELECTRIC = 2, RT_CHECKERBOARD = 3, RT_LIGHT = 4 };
+/* Integrators behind Renderer::Tick (renderer.cpp:227-231). */
+enum { RT_MODE_PATH = 0 };
+
+/* One primitive, Primitive::create* factories (Primitive.h:690-747):
+ *   RT_SPHERE:   v[0..2] centre, v[3] radius
+ *   RT_PLANE:    v[0..2] normal, v[3] distance
+ *   RT_TRIANGLE: v[0..8] three world-space vertices (post Scene::LoadModel) */
+typedef struct { int32_t type; int32_t material; float v[9]; } rt_prim;
+
+/* One material.  color = Diffuse/Mirror/Light colour or Dielectric absorption;
+ * color2 = Checkerboard second colour; ior = Dielectric n; diffuse = Checkerboard
+ * diffuse share (< 0 selects the 2-argument constructor: diffuse 1, specular 0). */
+typedef struct { int32_t kind; float color[3]; float color2[3]; float ior; float diffuse; } rt_material;
+
+/* Scene description, the inputs of Scene::Scene (template/scene.h:40-128). */
+typedef struct {
+    const rt_prim *prims; uint32_t num_prims;
+    const rt_material *materials; uint32_t num_materials;
+    /* sky: power-of-two texture of 0x00RRGGBB (renderer.h:15-22); NULL = the
+     * synthetic 1024x512 constant 0x406080 sky of SURVEY.md 8(d) */
+    const uint32_t *sky_pixels; uint32_t sky_width, sky_height;
+    /* optional prebuilt plain BVH: nodes in the 32-byte BVHNode layout
+     * (BVHNode.h:5-14, root 0, node 1 unused) + primitiveIndices; NULL = build
+     * here with the reference's binned SAH (template/scene.h:845-976) */
+    const void *bvh_nodes; uint32_t bvh_num_nodes; const uint32_t *bvh_indices;
+    int32_t device;
+} rt_scene_desc;
+
+typedef struct { uint32_t num_prims, nodes_used, depth, max_leaf; } rt_scene_info;
+
+/* Ray / hit records of the batched entry points (Ray.h:7-32). */
+typedef struct { float ox, oy, oz, dx, dy, dz, tmax; } rt_ray;       /* 28 B */
+typedef struct { float t; int32_t obj; float u, v; } rt_hit;           /* 16 B */
+
+/* Camera state (camera.h:93-100): origin, virtual screen corners, lens radius. */
+typedef struct { float pos[3], top_left[3], top_right[3], bottom_left[3]; float lens_radius; } rt_camera;
+
+/* One frame.  spp samples per pixel per frame; depth = Trace depth (renderer.h:9
+ * default 10; depth 1 = primary + NEE shadow ray); frame feeds the per-pixel seed
+ * InitSeed(pixel + W*H*(sample + spp*frame)) (template/template.cpp:683-686);
+ * reset = clear the accumulator first (renderer.cpp:237). */
+typedef struct { uint32_t width, height, spp, depth, frame, mode, reset; } rt_frame_params;
+
+/* Cumulative ray counters of a renderer. */
+typedef struct { uint64_t primary, shadow, bounce, frames; } rt_counters;
+
+typedef struct rt_scene rt_scene;
+typedef struct rt_renderer rt_renderer;
+
+/* ---- library ---------------------------------------------------------- */
+int rt_abi_version(void);
+const char *rt_last_error(void);
+int rt_device_count(int *count);
+void rt_free(void *p);
+
+/* ---- host-side scene preparation (Scene::LoadModel, template/scene.h:156-201) ---- */
+/* tinyobj-compatible OBJ read (template/tiny_obj_loader.h, triangulate=true):
+ * vertices float[3*nv], faces int32[3*nt] in file order; free with rt_free. */
+int rt_obj_load(const char *path, float **verts, uint32_t *nv, int32_t **faces, uint32_t *nt);
+/* RTMESH1 container (parsed OBJ vertices + faces) used for the bundled scenes. */
+int rt_mesh_load(const char *path, float **verts, uint32_t *nv, int32_t **faces, uint32_t *nt);
+int rt_mesh_save(const char *path, const float *verts, uint32_t nv, const int32_t *faces, uint32_t nt);
+/* mat4 helpers, template/precomp.h:1007-1039 and template/template.cpp:779-792 */
+int rt_mat4_translate(float x, float y, float z, float out[16]);
+int rt_mat4_scale(float s, float out[16]);
+int rt_mat4_rotate(int axis, float angle, float out[16]);
+int rt_mat4_mul(const float a[16], const float b[16], float out[16]);
+/* append one triangle per face, vertices = TransformPosition(v, M)
+ * (template/scene.h:185-191); out holds nt rt_prim records */
+int rt_mesh_to_prims(const float *verts, uint32_t nv, const int32_t *faces, uint32_t nt,
+                     const float M[16], int32_t material, rt_prim *out);
+/* The SURVEY.md 8(d) scene recipes as descriptions: call once with prims == NULL to get
+ * the counts, then with arrays of that size. */
+int rt_recipe_describe(const char *name, const char *mesh_dir, rt_prim *prims, uint32_t *num_prims,
+                       rt_material *materials, uint32_t *num_materials);
+/* plain-BVH build only (no device): nodes (2N+2 x 32 B) and indices (N) */
+int rt_bvh_build_host(const rt_prim *prims, uint32_t n, void *nodes, uint32_t *indices, rt_scene_info *info);
+
+/* ---- scene (Scene, template/scene.h:37-1014) ------------------------------ */
+int rt_scene_create(const rt_scene_desc *desc, rt_scene **out);
+/* the SURVEY.md 8(d) scenes: "teapotF", "teapot", "mig16", "cfg3", "cfg5" */
+int rt_scene_create_recipe(const char *name, const char *mesh_dir, int32_t device, rt_scene **out);
+int rt_scene_destroy(rt_scene *s);
+int rt_scene_get_info(const rt_scene *s, rt_scene_info *info);
+/* host copy of the BVH in use (nodes_used x 32 B, num_prims x u32) */
+int rt_scene_copy_bvh(const rt_scene *s, void *nodes, uint32_t *indices);
+
+/* Batched Scene::IntersectBVH (template/scene.h:285-320): rays_dev[n] -> hits_dev[n]. */
+int rt_intersect(rt_scene *s, const rt_ray *rays_dev, rt_hit *hits_dev, uint32_t n, void *stream);
+/* Batched Scene::IsOccluded (template/scene.h:452-487): out_dev[i] = 1 if occluded. */
+int rt_occluded(rt_scene *s, const rt_ray *rays_dev, uint8_t *out_dev, uint32_t n, void *stream);
+/* Host-pointer conveniences of the two above (copy in, launch, copy out, sync). */
+int rt_intersect_host(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t n);
+int rt_occluded_host(rt_scene *s, const rt_ray *rays, uint8_t *out, uint32_t n);
+
+/* ---- renderer (Renderer, renderer.h:5-160) -------------------------------- */
+/* Camera::Camera (camera.h:28-41) for a W x H target */
+int rt_camera_default(uint32_t width, uint32_t height, rt_camera *out);
+int rt_renderer_create(rt_scene *s, uint32_t width, uint32_t height, rt_renderer **out);
+int rt_renderer_destroy(rt_renderer *r);
+/* Renderer::Tick (renderer.cpp:200-309): trace every pixel, running average into
+ * the float4 accumulator (235-241), RGBF32_to_RGB8 pack (template/precomp.h:432-448)
+ * into rgb8_dev[W*H] (0x00RRGGBB).  One kernel launch. */
+int rt_render_frame(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t *rgb8_dev, void *stream);
+/* Same as rt_render_frame, RGB8 delivered to host memory (the reference's
+ * screen->pixels, template/template.cpp:273-277); synchronous. */
+int rt_render_frame_host(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t *rgb8_host);
+/* Screen-tile shard of a frame: the 8x8 tiles t with t % num_shards == shard,
+ * packed as [tile][64] pixels into tiles_dev (rt_shard_capacity pixels). */
+int rt_shard_capacity(uint32_t width, uint32_t height, uint32_t num_shards, uint32_t *pixels);
+int rt_render_shard(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard,
+                    uint32_t num_shards, uint32_t *tiles_dev, void *stream);
+/* Rank-0 side of the per-frame gather: gathered_dev = num_shards consecutive shard
+ * buffers (each rt_shard_capacity pixels) -> rgb8_dev[W*H]. */
+int rt_assemble_shards(rt_renderer *r, const uint32_t *gathered_dev, uint32_t num_shards, uint32_t *rgb8_dev,
+                       void *stream);
+int rt_renderer_counters(rt_renderer *r, rt_counters *out);
+/* accumulator readback, W*H float4 */
+int rt_renderer_read_accumulator(rt_renderer *r, float *host_out);
+int rt_renderer_stream(rt_renderer *r, void **stream);
+int rt_synchronize(rt_renderer *r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,127 @@
+// rt_compat.hpp -- header-only C++ shim keeping the reference's class surface on top of
+// the librtamd.so C-ABI, so a host written against pmichels19/AdvancedGraphicsRayTracer's
+// Renderer / Scene / Camera / Ray (renderer.h, template/scene.h, camera.h, Ray.h) can
+// switch to the MI355X path by swapping includes.
+//
+//   Tmpl8::Ray                 Ray.h:7-32 (O, D, rD, t, objIdx, inside, u, v)
+//   Tmpl8::Scene::IntersectBVH template/scene.h:285   -> rt_intersect_host (batch of 1 or n)
+//   Tmpl8::Scene::IsOccluded   template/scene.h:452   -> rt_occluded_host
+//   Tmpl8::Camera              camera.h:28-52         -> rt_camera_default
+//   Tmpl8::Renderer::Tick      renderer.cpp:200-309   -> rt_render_frame_host
+//
+// Per-ray calls cross PCIe; batch them (the vector overloads) for throughput.  There is
+// no CPU fallback: every call reports the library's error through RtError.
+#pragma once
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "rt_amd.h"
+
+namespace Tmpl8 {
+
+struct RtError : std::runtime_error {
+    int code;
+    RtError(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+inline void rt_check(int rc) {
+    if (rc != RT_OK) throw RtError(rc, rt_last_error());
+}
+
+struct float3 { float x = 0, y = 0, z = 0; };
+
+class Ray {   // Ray.h:7-32
+  public:
+    Ray() = default;
+    Ray(float3 origin, float3 direction, float distance = 1e34f) : O(origin), D(direction), t(distance) {
+        rD = float3{1 / D.x, 1 / D.y, 1 / D.z};
+    }
+    float3 IntersectionPoint() const { return float3{O.x + t * D.x, O.y + t * D.y, O.z + t * D.z}; }
+    float3 O, D, rD;
+    float t = 1e34f;
+    int objIdx = -1;
+    bool inside = false;
+    float u = 0, v = 0;
+};
+
+class Scene {   // template/scene.h:37
+  public:
+    explicit Scene(const char *recipe, const char *mesh_dir, int device = 0) {
+        rt_check(rt_scene_create_recipe(recipe, mesh_dir, device, &h_));
+    }
+    explicit Scene(const rt_scene_desc &desc) { rt_check(rt_scene_create(&desc, &h_)); }
+    Scene(const Scene &) = delete;
+    Scene &operator=(const Scene &) = delete;
+    ~Scene() { rt_scene_destroy(h_); }
+
+    void IntersectBVH(Ray &ray) { std::vector<Ray *> one{&ray}; IntersectBVH(one); }
+    bool IsOccluded(Ray &ray) { std::vector<Ray *> one{&ray}; return IsOccluded(one)[0]; }
+
+    void IntersectBVH(std::vector<Ray *> &rays) {
+        std::vector<rt_ray> in = pack(rays);
+        std::vector<rt_hit> out(in.size());
+        rt_check(rt_intersect_host(h_, in.data(), out.data(), (uint32_t)in.size()));
+        for (size_t i = 0; i < rays.size(); ++i) {
+            rays[i]->t = out[i].t;
+            rays[i]->objIdx = out[i].obj;
+            rays[i]->u = out[i].u;
+            rays[i]->v = out[i].v;
+        }
+    }
+    std::vector<bool> IsOccluded(std::vector<Ray *> &rays) {
+        std::vector<rt_ray> in = pack(rays);
+        std::vector<uint8_t> out(in.size());
+        rt_check(rt_occluded_host(h_, in.data(), out.data(), (uint32_t)in.size()));
+        return std::vector<bool>(out.begin(), out.end());
+    }
+    rt_scene_info Info() const { rt_scene_info i{}; rt_check(rt_scene_get_info(h_, &i)); return i; }
+    rt_scene *handle() const { return h_; }
+
+  private:
+    rt_scene *h_ = nullptr;
+    static std::vector<rt_ray> pack(const std::vector<Ray *> &rays) {
+        std::vector<rt_ray> in(rays.size());
+        for (size_t i = 0; i < rays.size(); ++i) {
+            const Ray &r = *rays[i];
+            in[i] = rt_ray{r.O.x, r.O.y, r.O.z, r.D.x, r.D.y, r.D.z, r.t};
+        }
+        return in;
+    }
+};
+
+class Camera {   // camera.h:28-41
+  public:
+    Camera(uint32_t width, uint32_t height) { rt_check(rt_camera_default(width, height, &cam)); }
+    rt_camera cam{};
+};
+
+class Renderer {   // renderer.h:5-160
+  public:
+    Renderer(Scene &scene, uint32_t width, uint32_t height)
+        : scene(scene), camera(width, height), width_(width), height_(height), pixels(size_t(width) * height) {
+        rt_check(rt_renderer_create(scene.handle(), width, height, &h_));
+    }
+    Renderer(const Renderer &) = delete;
+    Renderer &operator=(const Renderer &) = delete;
+    ~Renderer() { rt_renderer_destroy(h_); }
+
+    // One frame: path trace (depth 10 by default, renderer.h:9), accumulate, pack into pixels.
+    void Tick(float /*deltaTime*/, uint32_t depth = 10, uint32_t spp = 1) {
+        rt_frame_params p{width_, height_, spp, depth, frame_++, RT_MODE_PATH, 0};
+        rt_check(rt_render_frame_host(h_, &camera.cam, &p, pixels.data()));
+    }
+    rt_counters Counters() { rt_counters c{}; rt_check(rt_renderer_counters(h_, &c)); return c; }
+
+    Scene &scene;
+    Camera camera;
+
+  private:
+    uint32_t width_, height_;
+    uint32_t frame_ = 0;
+    rt_renderer *h_ = nullptr;
+
+  public:
+    std::vector<uint32_t> pixels;   // 0x00RRGGBB, the reference's screen->pixels
+};
+
+}  // namespace Tmpl8

@@ -16,7 +16,8 @@ LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
 
 class Stats(C.Structure):
     _fields_ = [(n, C.c_int64) for n in
-                ("coverage", "shadow", "isect", "occl", "bf_tested", "bf_mismatch", "aabb_tests", "prim_tests")]
+                ("coverage", "shadow", "isect", "occl", "bf_tested", "bf_mismatch", "aabb_tests", "prim_tests",
+                 "aabb_occl", "prim_occl")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -67,6 +68,7 @@ def lib():
                                       fp, C.POINTER(Stats)]
         L.or_tick.argtypes = [vp, C.POINTER(Camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                               fp, C.POINTER(C.c_uint32), C.POINTER(Stats), C.c_int]
+        L.or_camera_rays.argtypes = [C.POINTER(Camera), C.c_int, C.c_int, C.c_int, ip, C.c_int, fp]
         L.or_intersect.argtypes = [vp, fp, C.c_int, fp, ip, fp, fp, C.c_int]
         L.or_occluded.argtypes = [vp, fp, C.c_int, C.POINTER(C.c_uint8)]
         L.or_obj_parse.argtypes = [C.c_char_p, C.POINTER(fp), ip, C.POINTER(ip), ip]
@@ -141,6 +143,13 @@ class Scene:
         cam = Camera()
         lib().or_camera_default(C.byref(cam), W, H)
         return cam
+
+    def camera_rays(self, W, H, pixels, frame=0):
+        pixels = np.ascontiguousarray(pixels, dtype=np.int32)
+        rays = np.empty((len(pixels), 7), np.float32)
+        cam = self.camera(W, H)
+        self.L.or_camera_rays(C.byref(cam), W, H, frame, _p(pixels, C.c_int32), len(pixels), _p(rays, C.c_float))
+        return rays
 
     def primary_hits(self, W, H, pixels, frame=0):
         pixels = np.ascontiguousarray(pixels, dtype=np.int32)

@@ -153,7 +153,7 @@ static inline ray_t mkray(f3 O, f3 D, float t) {
     return r;
 }
 
-typedef struct { int64_t aabb, prim, isect, occl, shadow; } counters;
+typedef struct { int64_t aabb, prim, isect, occl, shadow, aabb_o, prim_o; } counters;
 
 or_scene *or_scene_new(void) {
     or_scene *s = (or_scene *)calloc(1, sizeof(or_scene));
@@ -509,7 +509,7 @@ static int is_occluded(const or_scene *s, const ray_t *r, counters *k) {   /* 45
         if (n->count > 0) {
             for (uint32_t i = 0; i < n->count; i++) {
                 int oi = (int)s->idx[n->leftFirst + i];
-                if (k) k->prim++;
+                if (k) { k->prim++; k->prim_o++; }
                 if (prim_hit(&s->p[oi], r)) return 1;
             }
             if (sp == 0) break;
@@ -518,7 +518,7 @@ static int is_occluded(const or_scene *s, const ray_t *r, counters *k) {   /* 45
         }
         const node *c1 = &s->nodes[n->leftFirst], *c2 = &s->nodes[n->leftFirst + 1];
         int h1 = hits_aabb(r, c1), h2 = hits_aabb(r, c2);
-        if (k) k->aabb += 2;
+        if (k) { k->aabb += 2; k->aabb_o += 2; }
         if (h1 && h2) { n = c1; stack[sp++] = c2; }
         else if (!(h1 || h2)) { if (sp == 0) break; n = stack[--sp]; }
         else if (h1) n = c1;
@@ -759,6 +759,16 @@ static inline uint32_t pixel_seed(int W, int H, int pixel, int sample, int spp, 
     return or_init_seed((uint32_t)pixel + (uint32_t)W * (uint32_t)H * (uint32_t)(sample + spp * frame));
 }
 
+void or_camera_rays(const or_camera *c, int W, int H, int frame, const int32_t *pixels, int n, float *rays7) {
+    for (int i = 0; i < n; i++) {
+        int px = pixels[i];
+        uint32_t seed = pixel_seed(W, H, px, 0, 1, frame);
+        ray_t r = primary_ray(c, px % W, px / W, &seed);
+        float *q = rays7 + 7 * (size_t)i;
+        q[0] = r.O.x; q[1] = r.O.y; q[2] = r.O.z; q[3] = r.D.x; q[4] = r.D.y; q[5] = r.D.z; q[6] = r.t;
+    }
+}
+
 void or_primary_hits(const or_scene *s, const or_camera *c, int W, int H, int frame,
                      const int32_t *pixels, int n, float *t, int32_t *obj, float *u, float *v) {
     #pragma omp parallel for schedule(dynamic, 64)
@@ -783,6 +793,10 @@ static void add_counters(or_stats *st, const counters *k) {
     st->aabb_tests += k->aabb;
     #pragma omp atomic
     st->prim_tests += k->prim;
+    #pragma omp atomic
+    st->aabb_occl += k->aabb_o;
+    #pragma omp atomic
+    st->prim_occl += k->prim_o;
 }
 
 static f3 trace_pixel(const or_scene *s, const or_camera *c, int W, int H, int spp, int depth, int frame,
@@ -918,6 +932,7 @@ void or_probe(const or_scene *s, int W, int H, int mode, int depth, int spp, int
         }
     st->shadow = k.shadow; st->isect = k.isect; st->occl = k.occl;
     st->aabb_tests = k.aabb; st->prim_tests = k.prim;
+    st->aabb_occl = k.aabb_o; st->prim_occl = k.prim_o;
 }
 
 /* ------------------------------------------------------------------ OBJ parsing (tinyobj restatement) */

@@ -48,6 +48,8 @@ typedef struct {
     int64_t bf_mismatch; /* of those, objIdx disagreements */
     int64_t aabb_tests;  /* child AABB tests, all traversals */
     int64_t prim_tests;  /* primitive tests, all traversals */
+    int64_t aabb_occl;   /* of aabb_tests, those made by IsOccluded */
+    int64_t prim_occl;   /* of prim_tests, those made by IsOccluded */
 } or_stats;
 
 /* OBJ parsing: restates tinyobj LoadObj (template/tiny_obj_loader.h:2554-2830,
@@ -89,6 +91,8 @@ void or_camera_default(or_camera *c, int W, int H);
 
 /* hot path, per-pixel seeded: seed = InitSeed(pixel + W*H*(sample + spp*frame)) */
 uint32_t or_init_seed(uint32_t base);
+/* Camera::GetPrimaryRay for sample 0 of a pixel list -> rays7 (O.xyz D.xyz t) */
+void or_camera_rays(const or_camera *c, int W, int H, int frame, const int32_t *pixels, int n, float *rays7);
 void or_primary_hits(const or_scene *s, const or_camera *c, int W, int H, int frame,
                      const int32_t *pixels, int n, float *t, int32_t *obj, float *u, float *v);
 /* Renderer::Trace radiance averaged over spp for a pixel list (renderer.cpp:17-72, 222) */

@@ -331,9 +331,10 @@ class Scene:
         return cls(device=device, _handle=h)
 
     def close(self):
-        if getattr(self, "h", None) and self.h.value:
-            self.L.rt_scene_destroy(self.h)
-            self.h = C.c_void_p()
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            self.L.rt_scene_destroy(h)
+            self.h = None
 
     __del__ = close
 
@@ -403,9 +404,10 @@ class Renderer:
         self.frame = 0
 
     def close(self):
-        if getattr(self, "h", None) and self.h.value:
-            self.L.rt_renderer_destroy(self.h)
-            self.h = C.c_void_p()
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            self.L.rt_renderer_destroy(h)
+            self.h = None
 
     __del__ = close
 

@@ -641,7 +641,7 @@ int validate_bvh(const Bvh &b, uint32_t n) {
 void free_scene(rt_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
-    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    (void)hipDeviceSynchronize();
     void *ptrs[] = {s->d_nodes, s->d_prims, s->d_shade, s->d_mats, s->d_sky, s->d_scratch};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -873,7 +873,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     F.out = out;
     F.counters = r->d_counters;
     if (F.ntiles_local == 0) return RT_OK;
-    hipStream_t st = stream ? (hipStream_t)stream : r->stream;
+    hipStream_t st = (hipStream_t)stream;
     dim3 grid((F.ntiles_local + 3) / 4), block(256);
     const size_t lds = stack_bytes(s);
     const uint32_t depth = p->depth;
@@ -963,7 +963,7 @@ int rt_intersect(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t n, void
     if (!s || (n && (!rays || !hits))) return fail(RT_ERR_INVALID, "rt_intersect: null argument");
     if (n == 0) return RT_OK;
     HIP_TRY(hipSetDevice(s->device));
-    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(k_intersect, dim3((n + 255) / 256), dim3(256), stack_bytes(s), st, s->view, rays, hits, n);
     HIP_TRY(hipGetLastError());
     return RT_OK;
@@ -973,7 +973,7 @@ int rt_occluded(rt_scene *s, const rt_ray *rays, uint8_t *out, uint32_t n, void 
     if (!s || (n && (!rays || !out))) return fail(RT_ERR_INVALID, "rt_occluded: null argument");
     if (n == 0) return RT_OK;
     HIP_TRY(hipSetDevice(s->device));
-    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(k_occluded, dim3((n + 255) / 256), dim3(256), stack_bytes(s), st, s->view, rays, out, n);
     HIP_TRY(hipGetLastError());
     return RT_OK;
@@ -1015,14 +1015,16 @@ int rt_renderer_create(rt_scene *s, uint32_t W, uint32_t H, rt_renderer **out) {
     rt_renderer *r = new rt_renderer();
     r->scene = s;
     r->W = W; r->H = H;
-    hipError_t e = hipMalloc(&r->d_acc, sizeof(float4) * (size_t)W * H);   // Renderer::Init, renderer.cpp:6-12
-    if (e == hipSuccess) e = hipMemset(r->d_acc, 0, sizeof(float4) * (size_t)W * H);
+    hipError_t e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&r->d_acc, sizeof(float4) * (size_t)W * H);   // Renderer::Init, renderer.cpp:6-12
+    if (e == hipSuccess) e = hipMemsetAsync(r->d_acc, 0, sizeof(float4) * (size_t)W * H, r->stream);
     if (e == hipSuccess) e = hipMalloc(&r->d_counters, 4 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemset(r->d_counters, 0, 4 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMemsetAsync(r->d_counters, 0, 4 * sizeof(unsigned long long), r->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(r->stream);   // ready before any caller stream uses it
     if (e != hipSuccess) {
         if (r->d_acc) (void)hipFree(r->d_acc);
         if (r->d_counters) (void)hipFree(r->d_counters);
+        if (r->stream) (void)hipStreamDestroy(r->stream);
         delete r;
         return fail(RT_ERR_HIP, std::string("rt_renderer_create: ") + hipGetErrorString(e));
     }
@@ -1033,7 +1035,7 @@ int rt_renderer_create(rt_scene *s, uint32_t W, uint32_t H, rt_renderer **out) {
 int rt_renderer_destroy(rt_renderer *r) {
     if (!r) return RT_OK;
     (void)hipSetDevice(r->scene->device);
-    (void)hipStreamSynchronize(r->stream);
+    (void)hipDeviceSynchronize();   // kernels on caller streams may still read the buffers
     (void)hipFree(r->d_acc);
     (void)hipFree(r->d_counters);
     if (r->d_rgb) (void)hipFree(r->d_rgb);
@@ -1075,7 +1077,7 @@ int rt_assemble_shards(rt_renderer *r, const uint32_t *gathered, uint32_t nshard
     uint32_t cap = 0;
     rt_shard_capacity(r->W, r->H, nshards, &cap);
     uint32_t tiles_x = (r->W + 7) / 8, ntiles = tiles_x * ((r->H + 7) / 8);
-    hipStream_t st = stream ? (hipStream_t)stream : r->stream;
+    hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(k_assemble, dim3((ntiles + 3) / 4), dim3(256), 0, st, gathered, cap, nshards, tiles_x, ntiles,
                        r->W, r->H, rgb8);
     HIP_TRY(hipGetLastError());

@@ -14,8 +14,10 @@
  *   - scene/renderer handles are opaque; the library owns all device buffers it
  *     allocates; pointers named *_dev are caller-owned DEVICE memory, the rest are
  *     caller-owned host memory;
- *   - stream arguments are hipStream_t passed as void* (NULL = the library's stream
- *     of that handle);
+ *   - stream arguments are hipStream_t passed as void*; NULL is HIP's default (null)
+ *     stream, as everywhere in HIP.  Handles create and finish their own setup work
+ *     before returning; the *_host conveniences run on the handle's private stream
+ *     and synchronize it;
  *   - primitive ids follow creation order exactly as the reference's
  *     Primitive::objIdx (Primitive.h:37-38); the light is primitive 0 and must be a
  *     sphere (Scene::GetRandomLight, template/scene.h:225-227).

@@ -3,6 +3,8 @@ same seeded inputs.  Bars (north_star): hit-primitive ids bit-exact; t/u/v and p
 within 1e-4 (the kernels are built to be bit-exact, so most checks assert equality);
 RGB8 frames bit-exact; ray counters exact.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -71,7 +73,13 @@ def test_random_rays_closest_hit_and_occlusion(scenes, name):
     short = rays.copy()
     short[:, 6] = np.random.default_rng(3).uniform(0.0, 4.0, len(rays)).astype(np.float32)
     got = g.IsOccluded(short).cpu().numpy()
-    assert np.array_equal(got, o.occluded(short).astype(bool))
+    want = o.occluded(short).astype(bool)
+    bad = np.nonzero(got != want)[0]
+    if len(bad):
+        os.makedirs("gpurun_out", exist_ok=True)
+        np.save(f"gpurun_out/occl_mismatch_{name}.npy", short[bad])
+    assert len(bad) == 0, f"{len(bad)} occlusion mismatches, first rays {short[bad[:3]].tolist()} got {got[bad[:3]]}"
+
 
 
 def test_brute_force_agrees_with_bvh(scenes):

@@ -18,7 +18,7 @@ step() {
 for s in "$@"; do
     case "$s" in
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-        tests) step gpu_tests 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+        tests) step gpu_tests 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
         bench) step bench 600 python bench.py --steps 30 --warmup 5 ;;
         prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
         *) echo "unknown step $s" ;;

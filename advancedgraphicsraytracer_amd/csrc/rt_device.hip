@@ -55,6 +55,7 @@ struct SceneView {
     float light_r, light_r2, light_invr;
     int light_mat;
     uint32_t root_word;
+    int bounds_finite;                  // every node bound is a finite float
 };
 
 struct FrameArgs {
@@ -98,23 +99,41 @@ __device__ __forceinline__ uint32_t f2u_wrap(float f) {
 }
 
 // ------------------------------------------------------------------ slab tests (scene.h:414-450)
-__device__ __forceinline__ float slab_dist(const DRay &r, float4 a, float4 b) {
+// EXACT: the reference's std::min/std::max selects, NaN behaviour included.
+// FAST (chosen per wave when every active ray has a finite origin and finite 1/D and the
+// scene's node bounds are NaN-free): no slab product can then be NaN, and on non-NaN
+// inputs the selects equal IEEE minNum/maxNum up to the sign of a zero result, which no
+// consumer can observe (the values are only compared) -- so v_min3/v_max3 give the
+// identical decisions with a third of the instructions.
+template <bool FAST>
+__device__ __forceinline__ void slab(const DRay &r, float4 a, float4 b, float &tmn, float &tmx) {
     float tx1 = (a.x - r.O.x) * r.rD.x, tx2 = (a.w - r.O.x) * r.rD.x;
-    float tmn = smin(tx1, tx2), tmx = smax(tx1, tx2);
     float ty1 = (a.y - r.O.y) * r.rD.y, ty2 = (b.x - r.O.y) * r.rD.y;
-    tmn = smax(tmn, smin(ty1, ty2)); tmx = smin(tmx, smax(ty1, ty2));
     float tz1 = (a.z - r.O.z) * r.rD.z, tz2 = (b.y - r.O.z) * r.rD.z;
-    tmn = smax(tmn, smin(tz1, tz2)); tmx = smin(tmx, smax(tz1, tz2));
+    if (FAST) {
+        tmn = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+        tmx = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    } else {
+        tmn = smin(tx1, tx2); tmx = smax(tx1, tx2);
+        tmn = smax(tmn, smin(ty1, ty2)); tmx = smin(tmx, smax(ty1, ty2));
+        tmn = smax(tmn, smin(tz1, tz2)); tmx = smin(tmx, smax(tz1, tz2));
+    }
+}
+template <bool FAST>
+__device__ __forceinline__ float slab_dist(const DRay &r, float4 a, float4 b) {
+    float tmn, tmx;
+    slab<FAST>(r, a, b, tmn, tmx);
     return (tmx >= tmn && tmn < r.t && tmx > 0) ? tmn : 1e30f;
 }
+template <bool FAST>
 __device__ __forceinline__ bool slab_hit(const DRay &r, float4 a, float4 b) {
-    float tx1 = (a.x - r.O.x) * r.rD.x, tx2 = (a.w - r.O.x) * r.rD.x;
-    float tmn = smin(tx1, tx2), tmx = smax(tx1, tx2);
-    float ty1 = (a.y - r.O.y) * r.rD.y, ty2 = (b.x - r.O.y) * r.rD.y;
-    tmn = smax(tmn, smin(ty1, ty2)); tmx = smin(tmx, smax(ty1, ty2));
-    float tz1 = (a.z - r.O.z) * r.rD.z, tz2 = (b.y - r.O.z) * r.rD.z;
-    tmn = smax(tmn, smin(tz1, tz2)); tmx = smin(tmx, smax(tz1, tz2));
+    float tmn, tmx;
+    slab<FAST>(r, a, b, tmn, tmx);
     return tmx >= tmn && tmn < r.t && tmx > 0;
+}
+__device__ __forceinline__ bool ray_finite(const DRay &r) {
+    return isfinite(r.O.x) && isfinite(r.O.y) && isfinite(r.O.z) && isfinite(r.rD.x) && isfinite(r.rD.y) &&
+           isfinite(r.rD.z);
 }
 
 // ------------------------------------------------------------------ primitive tests (Primitive.h:64-279)
@@ -207,7 +226,8 @@ __device__ __forceinline__ void finish_uv(const SceneView &S, DRay &r) {
 
 // ------------------------------------------------------------------ traversal (scene.h:285-320, 452-487)
 // stk points at this lane's column of the LDS stack; entry i lives at stk[i * 256].
-__device__ __forceinline__ void closest_hit(const SceneView &S, DRay &r, uint32_t *stk) {
+template <bool FAST>
+__device__ __forceinline__ void closest_hit_t(const SceneView &S, DRay &r, uint32_t *stk) {
     uint32_t word = S.root_word;
     int sp = 0;
     for (;;) {
@@ -220,7 +240,7 @@ __device__ __forceinline__ void closest_hit(const SceneView &S, DRay &r, uint32_
         }
         const float4 *q = S.nodes + 2 * lf;
         float4 a0 = q[0], b0 = q[1], a1 = q[2], b1 = q[3];
-        float d1 = slab_dist(r, a0, b0), d2 = slab_dist(r, a1, b1);
+        float d1 = slab_dist<FAST>(r, a0, b0), d2 = slab_dist<FAST>(r, a1, b1);
         uint32_t w1 = __float_as_uint(b0.z), w2 = __float_as_uint(b1.z);
         if (d1 > d2) { float td = d1; d1 = d2; d2 = td; uint32_t tw = w1; w1 = w2; w2 = tw; }
         if (d1 == 1e30f) {
@@ -233,7 +253,8 @@ __device__ __forceinline__ void closest_hit(const SceneView &S, DRay &r, uint32_
     }
 }
 
-__device__ __forceinline__ bool occluded(const SceneView &S, const DRay &r, uint32_t *stk) {
+template <bool FAST>
+__device__ __forceinline__ bool occluded_t(const SceneView &S, const DRay &r, uint32_t *stk) {
     uint32_t word = S.root_word;
     int sp = 0;
     for (;;) {
@@ -247,7 +268,7 @@ __device__ __forceinline__ bool occluded(const SceneView &S, const DRay &r, uint
         }
         const float4 *q = S.nodes + 2 * lf;
         float4 a0 = q[0], b0 = q[1], a1 = q[2], b1 = q[3];
-        bool h1 = slab_hit(r, a0, b0), h2 = slab_hit(r, a1, b1);
+        bool h1 = slab_hit<FAST>(r, a0, b0), h2 = slab_hit<FAST>(r, a1, b1);
         uint32_t w1 = __float_as_uint(b0.z), w2 = __float_as_uint(b1.z);
         if (h1 && h2) { word = w1; stk[sp++ * 256] = w2; }
         else if (!(h1 || h2)) { if (sp == 0) return false; word = stk[--sp * 256]; }
@@ -255,9 +276,21 @@ __device__ __forceinline__ bool occluded(const SceneView &S, const DRay &r, uint
     }
 }
 
+__device__ __forceinline__ void closest_hit(const SceneView &S, DRay &r, uint32_t *stk) {
+    if (__all(S.bounds_finite && ray_finite(r))) closest_hit_t<true>(S, r, stk);
+    else closest_hit_t<false>(S, r, stk);
+}
+__device__ __forceinline__ bool occluded(const SceneView &S, const DRay &r, uint32_t *stk) {
+    if (__all(S.bounds_finite && ray_finite(r))) return occluded_t<true>(S, r, stk);
+    return occluded_t<false>(S, r, stk);
+}
+
 // ------------------------------------------------------------------ shading
+// TEX_SKY = false: every texel is equal (the synthetic sky), so the lookup's index is
+// irrelevant and the colour is the precomputed texel -- bit-identical, no atan2/acos.
+template <bool TEX_SKY>
 __device__ __forceinline__ f3 sky_color(const SceneView &S, f3 D) {   // renderer.h:15-22
-    if (S.sky_const) return mk(S.sky_rgb[0], S.sky_rgb[1], S.sky_rgb[2]);
+    if (!TEX_SKY) return mk(S.sky_rgb[0], S.sky_rgb[1], S.sky_rgb[2]);
     uint32_t u = f2u_wrap((float)S.sky_w * cr_atan2(D.z, D.x) * kINV2PI - 0.5f);
     uint32_t v = f2u_wrap((float)S.sky_h * cr_acos(D.y) * kINVPI - 0.5f);
     uint32_t p = S.sky[(u & (S.sky_w - 1)) + (v & (S.sky_h - 1)) * S.sky_w];
@@ -394,7 +427,7 @@ __device__ __forceinline__ f3 nee(const SceneView &S, f3 I, f3 N, f3 BRDF, uint3
 // Renderer::Trace (renderer.cpp:17-72) as a loop.  The recursion's result
 // BRDF * ((Trace * dot) / PDF) + Ld is folded innermost-first from per-level records,
 // so the float evaluation order is the reference's.
-template <int MAXD>
+template <int MAXD, bool TEX_SKY>
 __device__ f3 trace_path(const SceneView &S, DRay ray, int depth, uint32_t &seed, uint32_t *stk, uint32_t &nshadow,
                          uint32_t &nbounce) {
     f3 lv_mul[MAXD], lv_add[MAXD];
@@ -406,7 +439,7 @@ __device__ f3 trace_path(const SceneView &S, DRay ray, int depth, uint32_t &seed
     for (int d = depth; d > 0 && levels < MAXD; --d) {
         if (d != depth) ++nbounce;
         closest_hit(S, ray, stk);
-        if (ray.obj == -1) { term = sky_color(S, ray.D); break; }
+        if (ray.obj == -1) { term = sky_color<TEX_SKY>(S, ray.D); break; }
         f3 I = ray.O + ray.t * ray.D;
         float4 s0 = S.shade[2 * ray.obj], s1 = S.shade[2 * ray.obj + 1];
         uint32_t ptype = __float_as_uint(s1.x);
@@ -414,7 +447,7 @@ __device__ f3 trace_path(const SceneView &S, DRay ray, int depth, uint32_t &seed
         if (dot(N, ray.D) > 0) N = -N;                                 // Scene::GetNormal
         const DevMaterial &m = S.mats[__float_as_int(s0.w)];
         if (m.flag == F_LIGHT) { term = lastSpec ? mk(m.c0[0], m.c0[1], m.c0[2]) : mk(0, 0, 0); break; }
-        const bool last = (d == 1);
+        const bool last = MAXD == 1 || d == 1;   // MAXD 1: the bounce ray is never traced
         DRay out;
         bool spec = scatter(m, ray, I, N, out, seed, last);
         f3 albedo = mat_color(m, ray, I);
@@ -479,8 +512,11 @@ __device__ __forceinline__ uint32_t pack_rgb8(float4 a) {
 // One frame (Renderer::Tick, renderer.cpp:200-309): per pixel spp x Trace, running
 // average into the accumulator, RGB8 pack.  Wave w of workgroup b owns screen tile
 // (b*4 + w) * nshards + shard.
-template <int MAXD>
-__global__ __launch_bounds__(256) void k_render(SceneView S, FrameArgs F) {
+#ifndef RT_RENDER_WAVES_PER_SIMD
+#define RT_RENDER_WAVES_PER_SIMD 1
+#endif
+template <int MAXD, bool TEX_SKY>
+__global__ __launch_bounds__(256, RT_RENDER_WAVES_PER_SIMD) void k_render(SceneView S, FrameArgs F) {
     extern __shared__ uint32_t lds_stack[];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t local_tile = blockIdx.x * 4u + (tid >> 6);
@@ -495,7 +531,7 @@ __global__ __launch_bounds__(256) void k_render(SceneView S, FrameArgs F) {
         for (uint32_t s = 0; s < F.spp; ++s) {
             uint32_t seed = init_seed(px + F.W * F.H * (s + F.spp * F.frame));
             DRay ray = primary_ray(F, x, y, seed);
-            sum = sum + trace_path<MAXD>(S, ray, (int)F.depth, seed, stk, nshadow, nbounce);
+            sum = sum + trace_path<MAXD, TEX_SKY>(S, ray, (int)F.depth, seed, stk, nshadow, nbounce);
         }
         f3 res = (1.0f / (float)F.spp) * sum;
         float4 a = F.reset ? make_float4(0, 0, 0, 0) : F.acc[px];
@@ -840,6 +876,13 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     v.light_mat = L.material;
     const Node &root = s->bvh.nodes[0];
     v.root_word = (root.leftFirst << 8) | root.count;
+    v.bounds_finite = 1;
+    for (uint32_t i = 0; i < s->bvh.nodes_used && v.bounds_finite; ++i) {
+        if (i == 1) continue;
+        const Node &nd = s->bvh.nodes[i];
+        for (int c = 0; c < 3; ++c)
+            if (!std::isfinite(nd.mn[c]) || !std::isfinite(nd.mx[c])) v.bounds_finite = 0;
+    }
     *out = s;
     return RT_OK;
 }
@@ -877,11 +920,21 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     dim3 grid((F.ntiles_local + 3) / 4), block(256);
     const size_t lds = stack_bytes(s);
     const uint32_t depth = p->depth;
-    if (depth <= 1) hipLaunchKernelGGL(k_render<1>, grid, block, lds, st, s->view, F);
-    else if (depth <= 4) hipLaunchKernelGGL(k_render<4>, grid, block, lds, st, s->view, F);
-    else if (depth <= 10) hipLaunchKernelGGL(k_render<10>, grid, block, lds, st, s->view, F);
-    else if (depth <= 32) hipLaunchKernelGGL(k_render<32>, grid, block, lds, st, s->view, F);
-    else return fail(RT_ERR_UNSUPPORTED, "Trace depth above 32");
+    if (depth > 32) return fail(RT_ERR_UNSUPPORTED, "Trace depth above 32");
+    const int md = depth <= 1 ? 1 : depth <= 4 ? 4 : depth <= 10 ? 10 : 32;
+    const bool tex = !s->view.sky_const;
+#define RT_LAUNCH(MD, TX) hipLaunchKernelGGL((k_render<MD, TX>), grid, block, lds, st, s->view, F)
+    switch (md * 2 + (tex ? 1 : 0)) {
+    case 2: RT_LAUNCH(1, false); break;
+    case 3: RT_LAUNCH(1, true); break;
+    case 8: RT_LAUNCH(4, false); break;
+    case 9: RT_LAUNCH(4, true); break;
+    case 20: RT_LAUNCH(10, false); break;
+    case 21: RT_LAUNCH(10, true); break;
+    case 64: RT_LAUNCH(32, false); break;
+    default: RT_LAUNCH(32, true); break;
+    }
+#undef RT_LAUNCH
     HIP_TRY(hipGetLastError());
     // pixels covered by this launch (primary rays per sample)
     uint64_t px = (uint64_t)F.ntiles_local * 64u;

@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of librtamd.so builds in ONE process (cdna_hip_programming.md
+5.4 rule 24).  Each build is loaded RTLD_LOCAL through raw ctypes; rounds alternate
+between builds; the per-build median and min of the per-frame kernel time are printed.
+
+usage: ab.py LIB [LIB ...] [--scene teapotF] [--w 1920] [--h 1080] [--spp 1] [--depth 1]
+             [--rounds 7] [--frames 20] [--check]
+--check compares every build's RGB8 frame with the first build's (bit-exact).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import advancedgraphicsraytracer_amd as rt  # noqa: E402  (structs only)
+
+
+def load(path):
+    L = C.CDLL(os.path.abspath(path), mode=C.RTLD_LOCAL)
+    vp, u32 = C.c_void_p, C.c_uint32
+    L.rt_scene_create_recipe.argtypes = [C.c_char_p, C.c_char_p, C.c_int32, C.POINTER(vp)]
+    L.rt_renderer_create.argtypes = [vp, u32, u32, C.POINTER(vp)]
+    L.rt_render_frame.argtypes = [vp, C.POINTER(rt.Camera), C.POINTER(rt.FrameParams), vp, vp]
+    L.rt_camera_default.argtypes = [u32, u32, C.POINTER(rt.Camera)]
+    L.rt_renderer_counters.argtypes = [vp, C.POINTER(rt.Counters)]
+    L.rt_last_error.restype = C.c_char_p
+    return L
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--scene", default="teapotF")
+    ap.add_argument("--w", type=int, default=1920)
+    ap.add_argument("--h", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=1)
+    ap.add_argument("--depth", type=int, default=1)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--check", action="store_true")
+    a = ap.parse_args()
+    builds = []
+    for p in a.libs:
+        L = load(p)
+        sc, r = C.c_void_p(), C.c_void_p()
+        assert L.rt_scene_create_recipe(a.scene.encode(), rt.DATA_DIR.encode(), 0, C.byref(sc)) == 0, L.rt_last_error()
+        assert L.rt_renderer_create(sc, a.w, a.h, C.byref(r)) == 0, L.rt_last_error()
+        cam = rt.Camera()
+        L.rt_camera_default(a.w, a.h, C.byref(cam))
+        out = torch.zeros(a.w * a.h, dtype=torch.int32, device="cuda")
+        builds.append((p, L, sc, r, cam, out))
+    times = {p: [] for p in a.libs}
+    frame = 0
+    for rnd in range(a.rounds):
+        for p, L, sc, r, cam, out in builds:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            # warm + timed frames on the default stream
+            fp = rt.FrameParams(a.w, a.h, a.spp, a.depth, frame, 0, 0)
+            L.rt_render_frame(r, C.byref(cam), C.byref(fp), C.c_void_p(out.data_ptr()), None)
+            ev[0].record()
+            for k in range(a.frames):
+                fp = rt.FrameParams(a.w, a.h, a.spp, a.depth, frame + 1 + k, 0, 0)
+                rc = L.rt_render_frame(r, C.byref(cam), C.byref(fp), C.c_void_p(out.data_ptr()), None)
+                assert rc == 0, L.rt_last_error()
+            ev[1].record()
+            torch.cuda.synchronize()
+            times[p].append(ev[0].elapsed_time(ev[1]) / a.frames)
+        frame += a.frames + 1
+    res = {}
+    for p, L, sc, r, cam, out in builds:
+        c = rt.Counters()
+        L.rt_renderer_counters(r, C.byref(c))
+        t = np.array(times[p])
+        rays_per_frame = (c.primary + c.shadow + c.bounce) / max(1, c.frames)
+        res[os.path.basename(p)] = {"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(t.min()), 4),
+                                    "mrays_s": round(rays_per_frame / (np.median(t) * 1e-3) / 1e6, 1)}
+    if a.check:
+        ref = None
+        for p, L, sc, r, cam, out in builds:
+            fr = rt.FrameParams(a.w, a.h, a.spp, a.depth, 12345, 0, 1)
+            L.rt_render_frame(r, C.byref(cam), C.byref(fr), C.c_void_p(out.data_ptr()), None)
+            torch.cuda.synchronize()
+            img = out.cpu().numpy().copy()
+            if ref is None:
+                ref = img
+            res[os.path.basename(p)]["same_image_as_first"] = bool(np.array_equal(img, ref))
+    print(json.dumps({"scene": a.scene, "w": a.w, "h": a.h, "spp": a.spp, "depth": a.depth, "results": res}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

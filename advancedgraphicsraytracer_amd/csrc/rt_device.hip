@@ -56,6 +56,8 @@ struct SceneView {
     int light_mat;
     uint32_t root_word;
     int bounds_finite;                  // every node bound is a finite float
+    uint32_t stack_entries;             // LDS stack entries per lane
+    uint32_t node_f4;                   // node array size in float4s
 };
 
 struct FrameArgs {
@@ -225,9 +227,18 @@ __device__ __forceinline__ void finish_uv(const SceneView &S, DRay &r) {
 }
 
 // ------------------------------------------------------------------ traversal (scene.h:285-320, 452-487)
-// stk points at this lane's column of the LDS stack; entry i lives at stk[i * 256].
-template <bool FAST>
-__device__ __forceinline__ void closest_hit_t(const SceneView &S, DRay &r, uint32_t *stk) {
+// Where a traversal reads its nodes and keeps its stack: `nodes` is the global node array
+// or the workgroup's LDS copy of it; `stk` is this lane's column of the LDS stack, entry i
+// at stk[i * STRIDE] (STRIDE = workgroup size: consecutive lanes, consecutive banks).
+template <int STRIDE>
+struct Trav {
+    const float4 *nodes;
+    uint32_t *stk;
+};
+
+template <bool FAST, int STRIDE>
+__device__ __forceinline__ void closest_hit_t(const SceneView &S, const Trav<STRIDE> &T, DRay &r) {
+    uint32_t *stk = T.stk;
     uint32_t word = S.root_word;
     int sp = 0;
     for (;;) {
@@ -235,26 +246,27 @@ __device__ __forceinline__ void closest_hit_t(const SceneView &S, DRay &r, uint3
         if (cnt) {
             for (uint32_t k = lf; k < lf + cnt; ++k) prim_intersect(S, k, r);
             if (sp == 0) break;
-            word = stk[--sp * 256];
+            word = stk[--sp * STRIDE];
             continue;
         }
-        const float4 *q = S.nodes + 2 * lf;
+        const float4 *q = T.nodes + 2 * lf;
         float4 a0 = q[0], b0 = q[1], a1 = q[2], b1 = q[3];
         float d1 = slab_dist<FAST>(r, a0, b0), d2 = slab_dist<FAST>(r, a1, b1);
         uint32_t w1 = __float_as_uint(b0.z), w2 = __float_as_uint(b1.z);
         if (d1 > d2) { float td = d1; d1 = d2; d2 = td; uint32_t tw = w1; w1 = w2; w2 = tw; }
         if (d1 == 1e30f) {
             if (sp == 0) break;
-            word = stk[--sp * 256];
+            word = stk[--sp * STRIDE];
         } else {
             word = w1;
-            if (d2 != 1e30f) stk[sp++ * 256] = w2;
+            if (d2 != 1e30f) stk[sp++ * STRIDE] = w2;
         }
     }
 }
 
-template <bool FAST>
-__device__ __forceinline__ bool occluded_t(const SceneView &S, const DRay &r, uint32_t *stk) {
+template <bool FAST, int STRIDE>
+__device__ __forceinline__ bool occluded_t(const SceneView &S, const Trav<STRIDE> &T, const DRay &r) {
+    uint32_t *stk = T.stk;
     uint32_t word = S.root_word;
     int sp = 0;
     for (;;) {
@@ -263,26 +275,28 @@ __device__ __forceinline__ bool occluded_t(const SceneView &S, const DRay &r, ui
             for (uint32_t k = lf; k < lf + cnt; ++k)
                 if (prim_hit(S, k, r)) return true;
             if (sp == 0) return false;
-            word = stk[--sp * 256];
+            word = stk[--sp * STRIDE];
             continue;
         }
-        const float4 *q = S.nodes + 2 * lf;
+        const float4 *q = T.nodes + 2 * lf;
         float4 a0 = q[0], b0 = q[1], a1 = q[2], b1 = q[3];
         bool h1 = slab_hit<FAST>(r, a0, b0), h2 = slab_hit<FAST>(r, a1, b1);
         uint32_t w1 = __float_as_uint(b0.z), w2 = __float_as_uint(b1.z);
-        if (h1 && h2) { word = w1; stk[sp++ * 256] = w2; }
-        else if (!(h1 || h2)) { if (sp == 0) return false; word = stk[--sp * 256]; }
+        if (h1 && h2) { word = w1; stk[sp++ * STRIDE] = w2; }
+        else if (!(h1 || h2)) { if (sp == 0) return false; word = stk[--sp * STRIDE]; }
         else word = h1 ? w1 : w2;
     }
 }
 
-__device__ __forceinline__ void closest_hit(const SceneView &S, DRay &r, uint32_t *stk) {
-    if (__all(S.bounds_finite && ray_finite(r))) closest_hit_t<true>(S, r, stk);
-    else closest_hit_t<false>(S, r, stk);
+template <int STRIDE>
+__device__ __forceinline__ void closest_hit(const SceneView &S, const Trav<STRIDE> &T, DRay &r) {
+    if (__all(S.bounds_finite && ray_finite(r))) closest_hit_t<true>(S, T, r);
+    else closest_hit_t<false>(S, T, r);
 }
-__device__ __forceinline__ bool occluded(const SceneView &S, const DRay &r, uint32_t *stk) {
-    if (__all(S.bounds_finite && ray_finite(r))) return occluded_t<true>(S, r, stk);
-    return occluded_t<false>(S, r, stk);
+template <int STRIDE>
+__device__ __forceinline__ bool occluded(const SceneView &S, const Trav<STRIDE> &T, const DRay &r) {
+    if (__all(S.bounds_finite && ray_finite(r))) return occluded_t<true>(S, T, r);
+    return occluded_t<false>(S, T, r);
 }
 
 // ------------------------------------------------------------------ shading
@@ -393,7 +407,8 @@ __device__ __forceinline__ f3 mat_color(const DevMaterial &m, const DRay &in, f3
 }
 
 // Renderer::NextEventDirectIllumination, renderer.h:44-75 (light = prim 0, a sphere)
-__device__ __forceinline__ f3 nee(const SceneView &S, f3 I, f3 N, f3 BRDF, uint32_t &seed, uint32_t *stk,
+template <int STRIDE>
+__device__ __forceinline__ f3 nee(const SceneView &S, const Trav<STRIDE> &T, f3 I, f3 N, f3 BRDF, uint32_t &seed,
                                   uint32_t &nshadow) {
     f3 pt = mk(1, 1, 1);                                               // GetRandomPoint, Primitive.h:394-402
     while (dot(pt, pt) > 1) {
@@ -414,7 +429,7 @@ __device__ __forceinline__ f3 nee(const SceneView &S, f3 I, f3 N, f3 BRDF, uint3
     if (dotNL > 0 && dotNlL > 0) {
         DRay sh = make_ray(I, L, dist - 2.0f * kEPS);
         ++nshadow;
-        if (!occluded(S, sh, stk)) {
+        if (!occluded(S, T, sh)) {
             float solid = (dotNlL * area) / (dist * dist);
             float lightPDF = 1.0f / solid;
             const DevMaterial &lm = S.mats[S.light_mat];
@@ -427,9 +442,9 @@ __device__ __forceinline__ f3 nee(const SceneView &S, f3 I, f3 N, f3 BRDF, uint3
 // Renderer::Trace (renderer.cpp:17-72) as a loop.  The recursion's result
 // BRDF * ((Trace * dot) / PDF) + Ld is folded innermost-first from per-level records,
 // so the float evaluation order is the reference's.
-template <int MAXD, bool TEX_SKY>
-__device__ f3 trace_path(const SceneView &S, DRay ray, int depth, uint32_t &seed, uint32_t *stk, uint32_t &nshadow,
-                         uint32_t &nbounce) {
+template <int MAXD, bool TEX_SKY, int STRIDE>
+__device__ f3 trace_path(const SceneView &S, const Trav<STRIDE> &T, DRay ray, int depth, uint32_t &seed,
+                         uint32_t &nshadow, uint32_t &nbounce) {
     f3 lv_mul[MAXD], lv_add[MAXD];
     float lv_c[MAXD];
     bool lv_diff[MAXD];
@@ -438,7 +453,7 @@ __device__ f3 trace_path(const SceneView &S, DRay ray, int depth, uint32_t &seed
     bool lastSpec = true;
     for (int d = depth; d > 0 && levels < MAXD; --d) {
         if (d != depth) ++nbounce;
-        closest_hit(S, ray, stk);
+        closest_hit(S, T, ray);
         if (ray.obj == -1) { term = sky_color<TEX_SKY>(S, ray.D); break; }
         f3 I = ray.O + ray.t * ray.D;
         float4 s0 = S.shade[2 * ray.obj], s1 = S.shade[2 * ray.obj + 1];
@@ -453,7 +468,7 @@ __device__ f3 trace_path(const SceneView &S, DRay ray, int depth, uint32_t &seed
         f3 albedo = mat_color(m, ray, I);
         if (m.flag == F_DIFFUSE || (m.flag == F_MIX && !spec)) {
             f3 BRDF = albedo * kINVPI;
-            lv_add[levels] = nee(S, I, N, BRDF, seed, stk, nshadow);
+            lv_add[levels] = nee(S, T, I, N, BRDF, seed, nshadow);
             lv_mul[levels] = BRDF;
             lv_c[levels] = last ? 0.0f : dot(N, out.D);
             lv_diff[levels] = true;
@@ -509,29 +524,21 @@ __device__ __forceinline__ uint32_t pack_rgb8(float4 a) {
 }
 
 // ------------------------------------------------------------------ kernels
-// One frame (Renderer::Tick, renderer.cpp:200-309): per pixel spp x Trace, running
-// average into the accumulator, RGB8 pack.  Wave w of workgroup b owns screen tile
-// (b*4 + w) * nshards + shard.
-#ifndef RT_RENDER_WAVES_PER_SIMD
-#define RT_RENDER_WAVES_PER_SIMD 1
-#endif
-template <int MAXD, bool TEX_SKY>
-__global__ __launch_bounds__(256, RT_RENDER_WAVES_PER_SIMD) void k_render(SceneView S, FrameArgs F) {
-    extern __shared__ uint32_t lds_stack[];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t local_tile = blockIdx.x * 4u + (tid >> 6);
-    if (local_tile >= F.ntiles_local) return;
+// One screen tile (8x8, one wave) of one frame: per pixel spp x Trace, running average
+// into the accumulator (renderer.cpp:235-241), RGB8 pack; per-wave ray counters.
+template <int MAXD, bool TEX_SKY, int STRIDE>
+__device__ __forceinline__ void render_tile(const SceneView &S, const FrameArgs &F, const Trav<STRIDE> &T,
+                                            uint32_t local_tile, uint32_t lane) {
     const uint32_t tile = local_tile * F.nshards + F.shard;
     const uint32_t x = (tile % F.tiles_x) * 8u + (lane & 7u), y = (tile / F.tiles_x) * 8u + (lane >> 3);
     uint32_t nshadow = 0, nbounce = 0;
     if (x < F.W && y < F.H) {
-        uint32_t *stk = lds_stack + tid;
         const uint32_t px = x + y * F.W;
         f3 sum = mk(0, 0, 0);
         for (uint32_t s = 0; s < F.spp; ++s) {
             uint32_t seed = init_seed(px + F.W * F.H * (s + F.spp * F.frame));
             DRay ray = primary_ray(F, x, y, seed);
-            sum = sum + trace_path<MAXD, TEX_SKY>(S, ray, (int)F.depth, seed, stk, nshadow, nbounce);
+            sum = sum + trace_path<MAXD, TEX_SKY>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
         }
         f3 res = (1.0f / (float)F.spp) * sum;
         float4 a = F.reset ? make_float4(0, 0, 0, 0) : F.acc[px];
@@ -552,6 +559,39 @@ __global__ __launch_bounds__(256, RT_RENDER_WAVES_PER_SIMD) void k_render(SceneV
     }
 }
 
+// Global-node variant: 256-thread workgroups, wave w of workgroup b owns local tile b*4+w.
+#ifndef RT_RENDER_WAVES_PER_SIMD
+#define RT_RENDER_WAVES_PER_SIMD 1
+#endif
+template <int MAXD, bool TEX_SKY>
+__global__ __launch_bounds__(256, RT_RENDER_WAVES_PER_SIMD) void k_render(SceneView S, FrameArgs F) {
+    extern __shared__ uint32_t lds_stack[];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t local_tile = blockIdx.x * 4u + (tid >> 6);
+    if (local_tile >= F.ntiles_local) return;
+    Trav<256> T{S.nodes, lds_stack + tid};
+    render_tile<MAXD, TEX_SKY>(S, F, T, local_tile, tid & 63u);
+}
+
+// LDS-node variant for scenes whose node array fits beside the stacks (TEAPOT-F: 65 KB):
+// a 1024-thread workgroup copies the node array into LDS, then its 16 waves render 16
+// consecutive tiles (a 128x8 strip) reading every 64-byte sibling pair with ds_read_b128
+// instead of a vector-memory load.  One strip per workgroup leaves the balancing across
+// CUs to the hardware dispatcher: persistent grids with static or per-CU queues measured
+// 5-13 % slower (profiles/r01/ab_lds_*.json).  LDS = [stack_entries][1024] u32 | nodes.
+template <int MAXD, bool TEX_SKY>
+__global__ __launch_bounds__(1024) void k_render_lds(SceneView S, FrameArgs F) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t tid = threadIdx.x;
+    float4 *lnodes = reinterpret_cast<float4 *>(lds + S.stack_entries * 1024u);
+    for (uint32_t i = tid; i < S.node_f4; i += 1024u) lnodes[i] = S.nodes[i];
+    __syncthreads();
+    const uint32_t local_tile = blockIdx.x * 16u + (tid >> 6);
+    if (local_tile >= F.ntiles_local) return;
+    Trav<1024> T{lnodes, lds + tid};
+    render_tile<MAXD, TEX_SKY>(S, F, T, local_tile, tid & 63u);
+}
+
 __global__ __launch_bounds__(256) void k_intersect(SceneView S, const rt_ray *__restrict__ rays, rt_hit *__restrict__ hits,
                                                    uint32_t n) {
     extern __shared__ uint32_t lds_stack[];
@@ -559,7 +599,8 @@ __global__ __launch_bounds__(256) void k_intersect(SceneView S, const rt_ray *__
     if (i >= n) return;
     rt_ray q = rays[i];
     DRay r = make_ray(mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), q.tmax);
-    closest_hit(S, r, lds_stack + threadIdx.x);
+    Trav<256> T{S.nodes, lds_stack + threadIdx.x};
+    closest_hit(S, T, r);
     finish_uv(S, r);
     rt_hit h;
     h.t = r.t; h.obj = r.obj; h.u = r.u; h.v = r.v;
@@ -573,7 +614,8 @@ __global__ __launch_bounds__(256) void k_occluded(SceneView S, const rt_ray *__r
     if (i >= n) return;
     rt_ray q = rays[i];
     DRay r = make_ray(mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), q.tmax);
-    out[i] = occluded(S, r, lds_stack + threadIdx.x) ? 1 : 0;
+    Trav<256> T{S.nodes, lds_stack + threadIdx.x};
+    out[i] = occluded(S, T, r) ? 1 : 0;
 }
 
 // rank-0 side of the per-frame gather: packed shard tiles -> row-major frame
@@ -608,6 +650,8 @@ struct rt_scene {
     Bvh bvh;
     uint32_t num_prims = 0;
     uint32_t stack_depth = 0;   // LDS stack entries per lane
+    bool lds_nodes = false;     // frame kernel keeps the node array in LDS (k_render_lds)
+    uint32_t num_cus = 256;     // persistent grid size of k_render_lds
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
     void *d_scratch = nullptr;  // staging for the host-pointer batched calls
     size_t scratch_bytes = 0;
@@ -876,6 +920,16 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     v.light_mat = L.material;
     const Node &root = s->bvh.nodes[0];
     v.root_word = (root.leftFirst << 8) | root.count;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, s->device) == hipSuccess && prop.multiProcessorCount > 0)
+            s->num_cus = (uint32_t)prop.multiProcessorCount;
+    }
+    v.stack_entries = s->stack_depth;
+    v.node_f4 = 2u * s->bvh.nodes_used;
+#ifndef RT_DISABLE_LDS_SCENE
+    s->lds_nodes = (size_t)s->stack_depth * 4096u + (size_t)s->bvh.nodes_used * 32u <= 160u * 1024u;
+#endif
     v.bounds_finite = 1;
     for (uint32_t i = 0; i < s->bvh.nodes_used && v.bounds_finite; ++i) {
         if (i == 1) continue;
@@ -888,6 +942,10 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 }
 
 size_t stack_bytes(const rt_scene *s) { return (size_t)s->stack_depth * 256u * sizeof(uint32_t); }
+// k_render_lds: [stack_entries][1024] u32 stacks, then the node array
+size_t lds_scene_bytes(const rt_scene *s) {
+    return (size_t)s->stack_depth * 1024u * sizeof(uint32_t) + (size_t)s->bvh.nodes_used * 32u;
+}
 
 int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
                   uint32_t *out, int packed, void *stream) {
@@ -917,13 +975,30 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     F.counters = r->d_counters;
     if (F.ntiles_local == 0) return RT_OK;
     hipStream_t st = (hipStream_t)stream;
-    dim3 grid((F.ntiles_local + 3) / 4), block(256);
-    const size_t lds = stack_bytes(s);
     const uint32_t depth = p->depth;
     if (depth > 32) return fail(RT_ERR_UNSUPPORTED, "Trace depth above 32");
     const int md = depth <= 1 ? 1 : depth <= 4 ? 4 : depth <= 10 ? 10 : 32;
     const bool tex = !s->view.sky_const;
-#define RT_LAUNCH(MD, TX) hipLaunchKernelGGL((k_render<MD, TX>), grid, block, lds, st, s->view, F)
+    // LDS nodes pay off where registers allow 1024-thread workgroups without spilling:
+    // the primary+shadow kernel with the constant sky (103 VGPRs); the path-tracing
+    // variants keep the 256-thread global-node kernel (A/B in profiles/r01).
+    const bool use_lds = s->lds_nodes && md == 1 && !tex;
+    dim3 grid, block;
+    size_t lds;
+    if (use_lds) {
+        grid = dim3((F.ntiles_local + 15) / 16);
+        block = dim3(1024);
+        lds = lds_scene_bytes(s);
+    } else {
+        grid = dim3((F.ntiles_local + 3) / 4);
+        block = dim3(256);
+        lds = stack_bytes(s);
+    }
+#define RT_LAUNCH(MD, TX)                                                                       \
+    do {                                                                                        \
+        if (use_lds) hipLaunchKernelGGL((k_render_lds<MD, TX>), grid, block, lds, st, s->view, F); \
+        else hipLaunchKernelGGL((k_render<MD, TX>), grid, block, lds, st, s->view, F);             \
+    } while (0)
     switch (md * 2 + (tex ? 1 : 0)) {
     case 2: RT_LAUNCH(1, false); break;
     case 3: RT_LAUNCH(1, true); break;

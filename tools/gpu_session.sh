@@ -17,8 +17,8 @@ step() {
 }
 for s in "$@"; do
     case "$s" in
-        smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-        tests) step gpu_tests 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+        smoke) step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        tests) step gpu_tests 300 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
         bench) step bench 600 python bench.py --steps 30 --warmup 5 ;;
         prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
         pmc)

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librtamd.so")
 SOURCES = ["rt_host.cpp", "rt_device.hip"]
-HEADERS = ["rt_math.h", "rt_internal.h", os.path.join("..", "..", "include", "rt_amd.h")]
+HEADERS = ["rt_math.h", "rt_internal.h", "rt_libm.h", os.path.join("..", "..", "include", "rt_amd.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off + IEEE div/sqrt (hipcc's default) keep the kernels' float results

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "rt_internal.h"
+#include "rt_libm.h"
 
 namespace rt {
 
@@ -86,10 +87,8 @@ __device__ __forceinline__ DRay make_ray(f3 O, f3 D, float t) {   // Ray.h:9-16
     return r;
 }
 
-// correctly rounded float transcendentals (double evaluation, matching the oracle)
-__device__ __forceinline__ float cr_cos(float x) { return (float)cos((double)x); }
-__device__ __forceinline__ float cr_sin(float x) { return (float)sin((double)x); }
-__device__ __forceinline__ float cr_exp(float x) { return (float)exp((double)x); }
+// cold-path transcendentals (textured sky, sphere u/v): correctly rounded float via the
+// double functions, as the oracle does; the hot cos/sin/exp come from rt_libm.h
 __device__ __forceinline__ float cr_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
 __device__ __forceinline__ float cr_acos(float x) { return (float)acos((double)x); }
 __device__ __forceinline__ float cr_asin(float x) { return (float)asin((double)x); }
@@ -315,7 +314,9 @@ __device__ __forceinline__ f3 sky_color(const SceneView &S, f3 D) {   // rendere
 __device__ __forceinline__ f3 diffuse_dir(f3 N, uint32_t &seed) {
     float r0 = rnd_f(seed), r1 = rnd_f(seed);
     float r = sqrtf(r0), theta = kTWOPI * r1;
-    float x = r * cr_cos(theta), y = r * cr_sin(theta), z = sqrtf(1 - r0);
+    float st, ct;
+    sincos_f(theta, st, ct);
+    float x = r * ct, y = r * st, z = sqrtf(1 - r0);
     f3 a0 = mk(0.0f, -1.0f, 0.0f), a1 = mk(-1.0f, 0.0f, 0.0f);
     if (N.z + 1.0f > kFLT_EPSILON) {
         float a = 1.0f / (1.0f + N.z);
@@ -395,7 +396,7 @@ __device__ __forceinline__ bool scatter(const DevMaterial &m, const DRay &in, f3
 __device__ __forceinline__ f3 mat_color(const DevMaterial &m, const DRay &in, f3 I) {
     if (m.kind == RT_DIELECTRIC) {                                     // Dielectric.h:12-21
         f3 c = mk(1, 1, 1);
-        if (in.inside) { c.x = cr_exp(-m.c0[0] * in.t); c.y = cr_exp(-m.c0[1] * in.t); c.z = cr_exp(-m.c0[2] * in.t); }
+        if (in.inside) { c.x = exp_f(-m.c0[0] * in.t); c.y = exp_f(-m.c0[1] * in.t); c.z = exp_f(-m.c0[2] * in.t); }
         return c;
     }
     if (m.kind == RT_CHECKERBOARD) {                                   // Checkerboard.h:28-37
@@ -994,12 +995,9 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         block = dim3(256);
         lds = stack_bytes(s);
     }
-#define RT_LAUNCH(MD, TX)                                                                       \
-    do {                                                                                        \
-        if (use_lds) hipLaunchKernelGGL((k_render_lds<MD, TX>), grid, block, lds, st, s->view, F); \
-        else hipLaunchKernelGGL((k_render<MD, TX>), grid, block, lds, st, s->view, F);             \
-    } while (0)
-    switch (md * 2 + (tex ? 1 : 0)) {
+#define RT_LAUNCH(MD, TX) hipLaunchKernelGGL((k_render<MD, TX>), grid, block, lds, st, s->view, F)
+    if (use_lds) hipLaunchKernelGGL((k_render_lds<1, false>), grid, block, lds, st, s->view, F);
+    else switch (md * 2 + (tex ? 1 : 0)) {
     case 2: RT_LAUNCH(1, false); break;
     case 3: RT_LAUNCH(1, true); break;
     case 8: RT_LAUNCH(4, false); break;

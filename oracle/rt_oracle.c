@@ -62,10 +62,62 @@ static inline f3 fmin3(f3 a, f3 b) { return mk(tmin_(a.x, b.x), tmin_(a.y, b.y),
 static inline f3 fmax3(f3 a, f3 b) { return mk(tmax_(a.x, b.x), tmax_(a.y, b.y), tmax_(a.z, b.z)); }
 static inline float comp(f3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 
-/* correctly rounded float transcendentals via double */
-static inline float cr_cosf(float x) { return (float)cos((double)x); }
-static inline float cr_sinf(float x) { return (float)sin((double)x); }
-static inline float cr_expf(float x) { return (float)exp((double)x); }
+/* In-path cosf/sinf/expf (ObjectMaterial.h:32-33, Dielectric.h:15-17): double evaluation of
+ * fdlibm's minimax kernels with basic operations only, rounded once to float -- the same
+ * operation sequence as the kernels' csrc/rt_libm.h, so both sides agree bit for bit. */
+static inline double rint_small(double v) { const double sh = 6755399441055744.0; return (v + sh) - sh; }
+static inline double ksin(double x) {
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    double z = x * x, v = z * x;
+    double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    return x + v * (S1 + z * r);
+}
+static inline double kcos(double x) {
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    double z = x * x;
+    double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    double hz = 0.5 * z, w = 1.0 - hz;
+    return w + (((1.0 - w) - hz) + z * r);
+}
+static inline void sincos_f(float a, float *s, float *c) {
+    const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
+                 pio2_1t = 6.07710050650619224932e-11;
+    double x = (double)a;
+    double k = rint_small(x * invpio2);
+    double r = (x - k * pio2_1) - k * pio2_1t;
+    double sr = ksin(r), cr = kcos(r);
+    int q = (int)k & 3;
+    *s = (float)(q == 0 ? sr : q == 1 ? cr : q == 2 ? -sr : -cr);
+    *c = (float)(q == 0 ? cr : q == 1 ? -sr : q == 2 ? -cr : sr);
+}
+static inline float exp_f(float a) {
+    if (!(a == a)) return a;
+    if (a > 88.8f) return 1.0f / 0.0f;
+    if (a < -104.0f) return 0.0f;
+    const double ln2hi = 6.93147180369123816490e-01, ln2lo = 1.90821492927058770002e-10,
+                 invln2 = 1.44269504088896338700e+00;
+    const double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+                 P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+                 P5 = 4.13813679705723846039e-08;
+    double x = (double)a;
+    double k = rint_small(x * invln2);
+    double hi = x - k * ln2hi, lo = k * ln2lo;
+    double r = hi - lo, t = r * r;
+    double cc = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    double y = 1.0 - ((lo - (r * cc) / (2.0 - cc)) - hi);
+    uint64_t bits = (uint64_t)((int64_t)k + 1023) << 52;
+    double p;
+    memcpy(&p, &bits, 8);
+    return (float)(y * p);
+}
+static inline float cr_cosf(float x) { float s, c; sincos_f(x, &s, &c); return c; }
+static inline float cr_sinf(float x) { float s, c; sincos_f(x, &s, &c); return s; }
+static inline float cr_expf(float x) { return exp_f(x); }
+/* cold-path transcendentals (textured sky, sphere u/v): correctly rounded via libm double */
 static inline float cr_atan2f(float y, float x) { return (float)atan2((double)y, (double)x); }
 static inline float cr_acosf(float x) { return (float)acos((double)x); }
 static inline float cr_asinf(float x) { return (float)asin((double)x); }

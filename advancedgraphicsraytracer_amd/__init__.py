@@ -25,6 +25,8 @@ RT_OK, RT_ERR_INVALID, RT_ERR_NO_DEVICE, RT_ERR_HIP, RT_ERR_IO, RT_ERR_UNSUPPORT
 SPHERE, PLANE, TRIANGLE = 0, 1, 4
 DIFFUSE, MIRROR, DIELECTRIC, CHECKERBOARD, LIGHT = 0, 1, 2, 3, 4
 MODE_PATH = 0
+MODE_WHITTED = 1
+DEFAULT_DEPTH = {MODE_PATH: 10, MODE_WHITTED: 20}   # renderer.h:9, renderer.h:13
 RECIPES = ("teapotF", "teapot", "mig16", "cfg3", "cfg5")
 
 
@@ -402,6 +404,11 @@ class Renderer:
         self.h = C.c_void_p()
         _check(self.L.rt_renderer_create(scene.h, width, height, C.byref(self.h)))
         self.frame = 0
+        self.useWhitted = False   # renderer.h:158; toggled by the K key (renderer.h:138)
+
+    @property
+    def mode(self):
+        return MODE_WHITTED if self.useWhitted else MODE_PATH
 
     def close(self):
         h = getattr(self, "h", None)
@@ -411,11 +418,13 @@ class Renderer:
 
     __del__ = close
 
-    def params(self, spp=1, depth=10, frame=None, reset=False):
-        return FrameParams(self.width, self.height, spp, depth, self.frame if frame is None else frame, MODE_PATH,
+    def params(self, spp=1, depth=None, frame=None, reset=False):
+        mode = self.mode
+        depth = DEFAULT_DEPTH[mode] if depth is None else depth
+        return FrameParams(self.width, self.height, spp, depth, self.frame if frame is None else frame, mode,
                            int(reset))
 
-    def Tick(self, out=None, spp=1, depth=10, frame=None, reset=False, stream=None):
+    def Tick(self, out=None, spp=1, depth=None, frame=None, reset=False, stream=None):
         """Renderer::Tick: trace, accumulate, pack RGB8 into out (torch uint32/int32 [H*W] on device)."""
         torch = _torch()
         if out is None:
@@ -428,7 +437,7 @@ class Renderer:
             self.frame += 1
         return out
 
-    def tick_host(self, spp=1, depth=10, frame=None, reset=False):
+    def tick_host(self, spp=1, depth=None, frame=None, reset=False):
         """Renderer::Tick with the RGB8 frame returned in host memory (numpy uint32 [H*W])."""
         out = np.zeros(self.width * self.height, np.uint32)
         p = self.params(spp, depth, frame, reset)
@@ -442,7 +451,7 @@ class Renderer:
         _check(self.L.rt_shard_capacity(self.width, self.height, num_shards, C.byref(n)))
         return n.value
 
-    def render_shard(self, out, shard, num_shards, spp=1, depth=10, frame=None, reset=False, stream=None):
+    def render_shard(self, out, shard, num_shards, spp=1, depth=None, frame=None, reset=False, stream=None):
         torch = _torch()
         p = self.params(spp, depth, frame, reset)
         s = stream if stream is not None else torch.cuda.current_stream(out.device).cuda_stream

@@ -407,18 +407,23 @@ __device__ __forceinline__ f3 mat_color(const DevMaterial &m, const DRay &in, f3
     return mk(m.c0[0], m.c0[1], m.c0[2]);
 }
 
-// Renderer::NextEventDirectIllumination, renderer.h:44-75 (light = prim 0, a sphere)
-template <int STRIDE>
-__device__ __forceinline__ f3 nee(const SceneView &S, const Trav<STRIDE> &T, f3 I, f3 N, f3 BRDF, uint32_t &seed,
-                                  uint32_t &nshadow) {
-    f3 pt = mk(1, 1, 1);                                               // GetRandomPoint, Primitive.h:394-402
+// Scene::GetLightPos = Primitive::GetRandomPoint of the light sphere (Primitive.h:394-402)
+__device__ __forceinline__ f3 light_point(const SceneView &S, uint32_t &seed) {
+    f3 pt = mk(1, 1, 1);
     while (dot(pt, pt) > 1) {
         float x = rnd_f(seed) * 2.0f - 1.0f;
         float y = rnd_f(seed) * 2.0f - 1.0f;
         float z = rnd_f(seed) * 2.0f - 1.0f;
         pt = mk(x, y, z);
     }
-    f3 Il = tpos(S.light_M, normalize(pt) * S.light_r);
+    return tpos(S.light_M, normalize(pt) * S.light_r);
+}
+
+// Renderer::NextEventDirectIllumination, renderer.h:44-75 (light = prim 0, a sphere)
+template <int STRIDE>
+__device__ __forceinline__ f3 nee(const SceneView &S, const Trav<STRIDE> &T, f3 I, f3 N, f3 BRDF, uint32_t &seed,
+                                  uint32_t &nshadow) {
+    f3 Il = light_point(S, seed);
     float area = 4.0f * kPI * S.light_r2;                              // GetArea, Primitive.h:452
     f3 L = Il - I;
     float dist = length(L);
@@ -490,6 +495,167 @@ __device__ f3 trace_path(const SceneView &S, const Trav<STRIDE> &T, DRay ray, in
     return r;
 }
 
+// ------------------------------------------------------------------ Whitted (the K key)
+// ObjectMaterial::getColorModifier overrides: colour in c, colorVars[3] in c3 and the
+// refraction direction colorVars[4..6] in T (Diffuse.h:21-23, Mirror.h:21-23,
+// Light.h:20-22, Checkerboard.h:60-71, Dielectric.h:56-85).
+__device__ __forceinline__ void color_modifier(const DevMaterial &m, const DRay &in, f3 I, f3 N, f3 &c, float &c3,
+                                               f3 &T) {
+    c3 = 0.0f;
+    T = mk(0, 0, 0);
+    switch (m.kind) {
+    case RT_LIGHT:   // clamp = fmaxf(a, fminf(f, b)), template/precomp.h:782
+        c = mk(fmaxf(0.0f, fminf(m.c0[0], 1.0f)), fmaxf(0.0f, fminf(m.c0[1], 1.0f)), fmaxf(0.0f, fminf(m.c0[2], 1.0f)));
+        return;
+    case RT_CHECKERBOARD:
+        c = mat_color(m, in, I);
+        c3 = m.diffuse;
+        return;
+    case RT_DIELECTRIC: {
+        float n1 = 1, n2 = m.ior, n12 = n1 / n2;
+        float cosi = dot(N, in.D);
+        c = mk(1, 1, 1);
+        if (in.inside) {
+            c = mk(exp_f(-m.c0[0] * in.t), exp_f(-m.c0[1] * in.t), exp_f(-m.c0[2] * in.t));
+            n12 = 1 / n12;
+        }
+        float k = 1 - (n12 * n12) * (1 - (cosi * cosi));
+        if (k < 0) { c3 = -1.0f; return; }   // TIR
+        if (!in.inside) {
+            float sini = length(cross(N, in.D));
+            float sq = n12 * sini;
+            float cost = sqrtf(1 - sq * sq);
+            c3 = fresnel(n1, n2, cost, -cosi);
+        }
+        T = normalize(n12 * in.D - (n12 * cosi + sqrtf(k)) * N);
+        return;
+    }
+    default:
+        c = mk(m.c0[0], m.c0[1], m.c0[2]);
+        return;
+    }
+}
+
+// Renderer::DirectIllumination, renderer.h:24-42: 4 light-sphere samples, spotlight test
+// against GetLightDir (0,-1,0), GetLightColor (24,24,22) (template/scene.h:234-242).
+template <int STRIDE>
+__device__ __forceinline__ f3 direct_illumination(const SceneView &S, const Trav<STRIDE> &T, f3 I, f3 N,
+                                                  uint32_t &seed, uint32_t &nshadow) {
+    f3 result = mk(0, 0, 0);
+    const f3 ldir = mk(0.0f, -1.0f, 0.0f), lcol = mk(24.0f, 24.0f, 22.0f);
+    for (int i = 0; i < 4; ++i) {
+        f3 L = light_point(S, seed) - I;
+        float dist = length(L);
+        L = L / dist;
+        float dotDN = dot(L, N);
+        if (dotDN < 0 || dot(ldir, L) > 0) continue;
+        DRay sh = make_ray(I, L, dist - (2 * kEPS));
+        ++nshadow;
+        if (occluded(S, T, sh)) continue;
+        result = result + (dotDN / (dist * dist)) * lcol;
+    }
+    return result / 4.0f;
+}
+
+// Renderer::WhittedTrace (renderer.cpp:138-195) as a depth-first walk with an explicit
+// frame stack.  A frame holds the parent's colour modifier and its partial sum; a child's
+// value is added (scaled by Fr, Ft or 1 - diffuse) when it returns, and the dielectric's
+// refraction child starts only after the reflection child is finished -- the reference's
+// evaluation and RNG order, so results are bit-identical to the recursion.
+constexpr int kWHITTED_MAX = 32;
+struct WFrame {
+    f3 col, res, I, T;
+    float w, ft;
+    int flags;   // 1: scale the child by w, 2: refraction child pending, 4: its inside flag
+};
+
+template <bool TEX_SKY, int STRIDE>
+__device__ f3 trace_whitted(const SceneView &S, const Trav<STRIDE> &T, DRay ray, int depth, uint32_t &seed,
+                            uint32_t &nshadow, uint32_t &nbounce) {
+    WFrame st[kWHITTED_MAX];
+    int sp = 0;
+    bool primary = true;
+    for (;;) {
+        // ---- evaluate WhittedTrace(ray, depth - sp) up to its first child
+        f3 ret = mk(0, 0, 0);
+        if (depth - sp > 0) {
+            if (!primary) ++nbounce;
+            primary = false;
+            closest_hit(S, T, ray);
+            if (ray.obj == -1) {
+                ret = sky_color<TEX_SKY>(S, ray.D);
+            } else {
+                f3 I = ray.O + ray.t * ray.D;
+                float4 s0 = S.shade[2 * ray.obj], s1 = S.shade[2 * ray.obj + 1];
+                f3 N = __float_as_uint(s1.x) == T_SPH ? (I - mk(s0.x, s0.y, s0.z)) * s1.y : mk(s0.x, s0.y, s0.z);
+                if (dot(N, ray.D) > 0) N = -N;                         // Scene::GetNormal
+                const DevMaterial &m = S.mats[__float_as_int(s0.w)];
+                f3 col, Tdir;
+                float c3;
+                color_modifier(m, ray, I, N, col, c3, Tdir);
+                f3 res = mk(0, 0, 0);
+                WFrame f;
+                f.col = col; f.w = 1.0f; f.ft = 0.0f; f.flags = 0;
+                bool push = false, child_inside = false;
+                f3 childD = mk(0, 0, 0);
+                if (m.flag == F_LIGHT) {
+                    res = res + mk(24.0f, 24.0f, 22.0f);
+                } else if (m.flag == F_DIFFUSE) {
+                    res = res + direct_illumination(S, T, I, N, seed, nshadow);
+                } else if (m.flag == F_SPECULAR) {
+                    push = true; childD = normalize(reflect(ray.D, N));
+                } else if (m.flag == F_MIX) {
+                    res = res + c3 * direct_illumination(S, T, I, N, seed, nshadow);
+                    push = true; childD = normalize(reflect(ray.D, N));
+                    f.w = 1.0f - c3; f.flags = 1;
+                } else if (m.flag == F_DIELECTRIC) {
+                    if (c3 < 0) {
+                        push = true; childD = normalize(reflect(ray.D, N)); child_inside = true;
+                    } else {
+                        float Fr = c3, Ft = 1 - Fr;
+                        if (Fr > kFLT_EPSILON) {
+                            push = true; childD = normalize(reflect(ray.D, N));
+                            f.w = Fr; f.flags = 1;
+                            if (Ft > kFLT_EPSILON) {
+                                f.flags |= 2 | (ray.inside ? 0 : 4);
+                                f.ft = Ft; f.I = I; f.T = Tdir;
+                            }
+                        } else if (Ft > kFLT_EPSILON) {
+                            push = true; childD = Tdir; child_inside = !ray.inside;
+                            f.w = Ft; f.flags = 1;
+                        }
+                    }
+                }
+                if (push) {
+                    f.res = res;
+                    st[sp++] = f;
+                    ray = make_ray(I, childD, 1e34f);
+                    ray.inside = child_inside ? 1 : 0;
+                    continue;
+                }
+                ret = col * res;
+            }
+        }
+        // ---- return ret to the parents until one has a child left to trace
+        bool descend = false;
+        while (sp > 0) {
+            WFrame &f = st[sp - 1];
+            f.res = f.res + ((f.flags & 1) ? f.w * ret : ret);
+            if (f.flags & 2) {
+                ray = make_ray(f.I, f.T, 1e34f);
+                ray.inside = (f.flags & 4) ? 1 : 0;
+                f.w = f.ft;
+                f.flags &= ~2;
+                descend = true;
+                break;
+            }
+            ret = f.col * f.res;
+            --sp;
+        }
+        if (!descend) return ret;
+    }
+}
+
 // Camera::GetPrimaryRay (camera.h:43-52) + randomInUnitDisk (20-26)
 __device__ __forceinline__ DRay primary_ray(const FrameArgs &F, uint32_t x, uint32_t y, uint32_t &seed) {
     float u = (float)x * F.rw + rnd_f(seed) * F.rw;
@@ -525,7 +691,7 @@ __device__ __forceinline__ uint32_t pack_rgb8(float4 a) {
 }
 
 // ------------------------------------------------------------------ kernels
-// One screen tile (8x8, one wave) of one frame: per pixel spp x Trace, running average
+// One screen tile (8x8, one wave) of one frame: per pixel spp x Trace (MAXD = 0: WhittedTrace), running average
 // into the accumulator (renderer.cpp:235-241), RGB8 pack; per-wave ray counters.
 template <int MAXD, bool TEX_SKY, int STRIDE>
 __device__ __forceinline__ void render_tile(const SceneView &S, const FrameArgs &F, const Trav<STRIDE> &T,
@@ -539,7 +705,8 @@ __device__ __forceinline__ void render_tile(const SceneView &S, const FrameArgs 
         for (uint32_t s = 0; s < F.spp; ++s) {
             uint32_t seed = init_seed(px + F.W * F.H * (s + F.spp * F.frame));
             DRay ray = primary_ray(F, x, y, seed);
-            sum = sum + trace_path<MAXD, TEX_SKY>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
+            if constexpr (MAXD == 0) sum = sum + trace_whitted<TEX_SKY>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
+            else sum = sum + trace_path<MAXD, TEX_SKY>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
         }
         f3 res = (1.0f / (float)F.spp) * sum;
         float4 a = F.reset ? make_float4(0, 0, 0, 0) : F.acc[px];
@@ -954,7 +1121,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     if (p->width != r->W || p->height != r->H)
         return fail(RT_ERR_INVALID, "frame size differs from the renderer's accumulator");
     if (p->spp == 0) return fail(RT_ERR_INVALID, "spp must be >= 1");
-    if (p->mode != RT_MODE_PATH) return fail(RT_ERR_UNSUPPORTED, "only the path tracer (RT_MODE_PATH) is on the GPU path");
+    if (p->mode != RT_MODE_PATH && p->mode != RT_MODE_WHITTED) return fail(RT_ERR_INVALID, "unknown integrator mode");
     if (nshards == 0 || shard >= nshards) return fail(RT_ERR_INVALID, "bad shard index");
     rt_scene *s = r->scene;
     HIP_TRY(hipSetDevice(s->device));
@@ -977,8 +1144,8 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     if (F.ntiles_local == 0) return RT_OK;
     hipStream_t st = (hipStream_t)stream;
     const uint32_t depth = p->depth;
-    if (depth > 32) return fail(RT_ERR_UNSUPPORTED, "Trace depth above 32");
-    const int md = depth <= 1 ? 1 : depth <= 4 ? 4 : depth <= 10 ? 10 : 32;
+    if (depth > 32) return fail(RT_ERR_UNSUPPORTED, "Trace depth above 32");   // = kWHITTED_MAX
+    const int md = p->mode == RT_MODE_WHITTED ? 0 : depth <= 1 ? 1 : depth <= 4 ? 4 : depth <= 10 ? 10 : 32;
     const bool tex = !s->view.sky_const;
     // LDS nodes pay off where registers allow 1024-thread workgroups without spilling:
     // the primary+shadow kernel with the constant sky (103 VGPRs); the path-tracing
@@ -998,6 +1165,8 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
 #define RT_LAUNCH(MD, TX) hipLaunchKernelGGL((k_render<MD, TX>), grid, block, lds, st, s->view, F)
     if (use_lds) hipLaunchKernelGGL((k_render_lds<1, false>), grid, block, lds, st, s->view, F);
     else switch (md * 2 + (tex ? 1 : 0)) {
+    case 0: RT_LAUNCH(0, false); break;
+    case 1: RT_LAUNCH(0, true); break;
     case 2: RT_LAUNCH(1, false); break;
     case 3: RT_LAUNCH(1, true); break;
     case 8: RT_LAUNCH(4, false); break;

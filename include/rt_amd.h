@@ -48,8 +48,10 @@ enum {
 enum { RT_SPHERE = 0, RT_PLANE = 1, RT_TRIANGLE = 4 };
 /* Materials: Diffuse.h, Mirror.h, Dielectric.h, Checkerboard.h, Light.h. */
 enum { RT_DIFFUSE = 0, RT_MIRROR = 1, RT_DIELECTRIC = 2, RT_CHECKERBOARD = 3, RT_LIGHT = 4 };
-/* Integrators behind Renderer::Tick (renderer.cpp:227-231). */
-enum { RT_MODE_PATH = 0 };
+/* Integrators behind Renderer::Tick (renderer.cpp:227-231; the K key toggles them,
+ * renderer.h:138): Trace (path tracer, default depth 10, renderer.h:9) and WhittedTrace
+ * (default depth 20, renderer.h:13).  depth <= 32 for both. */
+enum { RT_MODE_PATH = 0, RT_MODE_WHITTED = 1 };
 
 /* One primitive, Primitive::create* factories (Primitive.h:690-747):
  *   RT_SPHERE:   v[0..2] centre, v[3] radius

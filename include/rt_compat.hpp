@@ -105,11 +105,17 @@ class Renderer {   // renderer.h:5-160
     Renderer &operator=(const Renderer &) = delete;
     ~Renderer() { rt_renderer_destroy(h_); }
 
-    // One frame: path trace (depth 10 by default, renderer.h:9), accumulate, pack into pixels.
-    void Tick(float /*deltaTime*/, uint32_t depth = 10, uint32_t spp = 1) {
-        rt_frame_params p{width_, height_, spp, depth, frame_++, RT_MODE_PATH, 0};
+    // One frame: Trace (depth 10, renderer.h:9) or WhittedTrace (depth 20, renderer.h:13)
+    // per pixel, accumulate, pack into pixels.  depth 0 = the reference's default.
+    void Tick(float /*deltaTime*/, uint32_t depth = 0, uint32_t spp = 1) {
+        if (depth == 0) depth = useWhitted ? 20 : 10;
+        rt_frame_params p{width_, height_, spp, depth, frame_++, useWhitted ? RT_MODE_WHITTED : RT_MODE_PATH,
+                          swapped_ ? 1u : 0u};
+        swapped_ = false;
         rt_check(rt_render_frame_host(h_, &camera.cam, &p, pixels.data()));
     }
+    // The K key (renderer.h:138): switch integrators; the next frame restarts accumulation.
+    void ToggleWhitted() { useWhitted = !useWhitted; swapped_ = true; }
     rt_counters Counters() { rt_counters c{}; rt_check(rt_renderer_counters(h_, &c)); return c; }
 
     Scene &scene;
@@ -118,9 +124,11 @@ class Renderer {   // renderer.h:5-160
   private:
     uint32_t width_, height_;
     uint32_t frame_ = 0;
+    bool swapped_ = false;
     rt_renderer *h_ = nullptr;
 
   public:
+    bool useWhitted = false;        // renderer.h:158
     std::vector<uint32_t> pixels;   // 0x00RRGGBB, the reference's screen->pixels
 };
 

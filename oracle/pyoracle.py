@@ -60,6 +60,7 @@ def lib():
         L.or_scene_add_sphere.argtypes = [vp, fp, C.c_float, C.c_int]
         L.or_scene_add_plane.argtypes = [vp, fp, C.c_float, C.c_int]
         L.or_scene_add_triangle.argtypes = [vp, fp, fp, fp, C.c_int]
+        L.or_scene_set_integrator.argtypes = [vp, C.c_int]
         L.or_scene_set_sky.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_uint32)]
         L.or_camera_default.argtypes = [C.POINTER(Camera), C.c_int, C.c_int]
         L.or_probe.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(Stats)]
@@ -111,6 +112,10 @@ class Scene:
         if getattr(self, "h", None):
             self.L.or_scene_free(self.h)
             self.h = None
+
+    def set_integrator(self, mode):
+        """0 = Renderer::Trace (path tracer), 1 = Renderer::WhittedTrace."""
+        self.L.or_scene_set_integrator(self.h, mode)
 
     @property
     def num_prims(self):

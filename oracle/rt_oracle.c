@@ -192,6 +192,7 @@ struct or_scene {
     node *nodes; int nodesUsed, depth;
     uint32_t *idx;
     int skyW, skyH; uint32_t *sky;
+    int integrator;   /* 0 = Renderer::Trace, 1 = Renderer::WhittedTrace (the K key, renderer.h:136-139) */
 };
 
 typedef struct {      /* Ray.h:7-32 */
@@ -806,6 +807,114 @@ static f3 trace(const or_scene *s, ray_t *ray, int lastSpecular, int depth, uint
     }
 }
 
+/* ObjectMaterial::getColorModifier overrides (Whitted colour + parameters):
+ * Diffuse.h:21-23, Mirror.h:21-23, Light.h:20-22, Checkerboard.h:60-71, Dielectric.h:56-85 */
+static void color_modifier(const material *m, const ray_t *in, f3 N, float cv[7]) {
+    memset(cv, 0, 7 * sizeof(float));
+    switch (m->kind) {
+    case OR_LIGHT:
+        /* template/precomp.h:782 clamp = fmaxf(a, fminf(f, b)) */
+        cv[0] = fmaxf(0.0f, fminf(m->c0.x, 1.0f)); cv[1] = fmaxf(0.0f, fminf(m->c0.y, 1.0f));
+        cv[2] = fmaxf(0.0f, fminf(m->c0.z, 1.0f));
+        return;
+    case OR_CHECKER: {
+        f3 c = mat_color(m, in);
+        cv[0] = c.x; cv[1] = c.y; cv[2] = c.z; cv[3] = m->diffuse;
+        return;
+    }
+    case OR_DIELECTRIC: {
+        float n1 = 1, n2 = m->ior, n12 = n1 / n2;
+        float cosi = dot(N, in->D);
+        f3 beers = mk(1, 1, 1);
+        if (in->inside) {
+            beers.x = cr_expf(-m->c0.x * in->t); beers.y = cr_expf(-m->c0.y * in->t); beers.z = cr_expf(-m->c0.z * in->t);
+            n12 = 1 / n12;
+        }
+        float k = 1 - (n12 * n12) * (1 - (cosi * cosi));
+        cv[0] = beers.x; cv[1] = beers.y; cv[2] = beers.z;
+        if (k < 0) { cv[3] = -1.0f; return; }
+        float Fr = 0;
+        if (!in->inside) {
+            float sini = length3(cross(N, in->D));
+            float sq = n12 * sini;
+            float cost = sqrtf(1 - sq * sq);
+            Fr = fresnel(n1, n2, cost, -cosi);
+        }
+        f3 T = normalize(sub(smul(n12, in->D), smul(n12 * cosi + sqrtf(k), N)));
+        cv[3] = Fr; cv[4] = T.x; cv[5] = T.y; cv[6] = T.z;
+        return;
+    }
+    default:
+        cv[0] = m->c0.x; cv[1] = m->c0.y; cv[2] = m->c0.z;
+        return;
+    }
+}
+
+/* Renderer::DirectIllumination, renderer.h:24-42 (4 light samples, GetLightDir (0,-1,0)) */
+static f3 direct_illumination(const or_scene *s, f3 I, f3 N, uint32_t *seed, counters *k) {
+    f3 result = mk(0, 0, 0);
+    int samples = 0;
+    const f3 ldir = mk(0.0f, -1.0f, 0.0f), lcol = mk(24, 24, 22);   /* scene.h:237-242 */
+    for (; samples < 4; samples++) {
+        f3 L = sub(light_random_point(&s->p[0], seed), I);
+        float dist = length3(L);
+        L = divs(L, dist);
+        float dotDN = dot(L, N);
+        if (dotDN < 0 || dot(ldir, L) > 0) continue;
+        ray_t toLight = mkray(I, L, dist - (2 * EPS_F));
+        if (k) k->shadow++;
+        if (is_occluded(s, &toLight, k)) continue;
+        result = add(result, smul(dotDN / (dist * dist), lcol));
+    }
+    return divs(result, (float)samples);
+}
+
+/* Renderer::WhittedTrace, renderer.cpp:138-195 */
+static f3 whitted(const or_scene *s, ray_t *ray, int depth, uint32_t *seed, counters *k) {
+    f3 result = mk(0, 0, 0);
+    if (depth == 0) return result;
+    intersect_bvh(s, ray, k);
+    if (ray->obj == -1) return sky_color(s, ray->D);
+    f3 I = add(ray->O, smul(ray->t, ray->D));
+    f3 N = scene_normal(s, ray->obj, I, ray->D);
+    const material *m = &s->m[s->p[ray->obj].mat];
+    int flag = mat_flag(m);
+    float cv[7];
+    color_modifier(m, ray, N, cv);
+    if (flag == FLAG_LIGHT) {
+        result = add(result, mk(24, 24, 22));
+    } else if (flag == FLAG_DIFFUSE) {
+        result = add(result, direct_illumination(s, I, N, seed, k));
+    } else if (flag == FLAG_SPECULAR) {
+        ray_t r = mkray(I, normalize(reflect(ray->D, N)), 1e34f);
+        result = add(result, whitted(s, &r, depth - 1, seed, k));
+    } else if (flag == FLAG_MIX) {
+        result = add(result, smul(cv[3], direct_illumination(s, I, N, seed, k)));
+        ray_t r = mkray(I, normalize(reflect(ray->D, N)), 1e34f);
+        result = add(result, smul(1.0f - cv[3], whitted(s, &r, depth - 1, seed, k)));
+    } else if (flag == FLAG_DIELECTRIC) {
+        if (cv[3] < 0) {
+            ray_t r = mkray(I, normalize(reflect(ray->D, N)), 1e34f);
+            r.inside = 1;
+            result = add(result, whitted(s, &r, depth - 1, seed, k));
+        } else {
+            float Fr = cv[3], Ft = 1 - Fr;
+            if (Fr > FLT_EPS_F) {
+                ray_t r = mkray(I, normalize(reflect(ray->D, N)), 1e34f);
+                result = add(result, smul(Fr, whitted(s, &r, depth - 1, seed, k)));
+            }
+            if (Ft > FLT_EPS_F) {
+                ray_t r = mkray(I, mk(cv[4], cv[5], cv[6]), 1e34f);
+                r.inside = !ray->inside;
+                result = add(result, smul(Ft, whitted(s, &r, depth - 1, seed, k)));
+            }
+        }
+    }
+    return mul(mk(cv[0], cv[1], cv[2]), result);
+}
+
+void or_scene_set_integrator(or_scene *s, int mode) { s->integrator = mode; }
+
 /* ------------------------------------------------------------------ drivers */
 static inline uint32_t pixel_seed(int W, int H, int pixel, int sample, int spp, int frame) {
     return or_init_seed((uint32_t)pixel + (uint32_t)W * (uint32_t)H * (uint32_t)(sample + spp * frame));
@@ -858,7 +967,7 @@ static f3 trace_pixel(const or_scene *s, const or_camera *c, int W, int H, int s
     for (int smp = 0; smp < spp; smp++) {
         uint32_t seed = pixel_seed(W, H, px, smp, spp, frame);
         ray_t r = primary_ray(c, x, y, &seed);
-        res = add(res, trace(s, &r, 1, depth, &seed, k));
+        res = add(res, s->integrator ? whitted(s, &r, depth, &seed, k) : trace(s, &r, 1, depth, &seed, k));
     }
     return smul(1.0f / (float)spp, res);
 }

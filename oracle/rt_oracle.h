@@ -86,6 +86,9 @@ or_scene *or_scene_recipe(const char *name, const char *mesh_dir);
 int or_mesh_read(const char *path, float **verts, int *nv, int **tris, int *nt);
 int or_mesh_write(const char *path, const float *verts, int nv, const int *tris, int nt);
 
+/* integrator used by or_trace_pixels / or_tick: 0 = Trace (default), 1 = WhittedTrace */
+void or_scene_set_integrator(or_scene *s, int mode);
+
 /* camera (camera.h:28-52) */
 void or_camera_default(or_camera *c, int W, int H);
 

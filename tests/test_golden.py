@@ -23,9 +23,12 @@ def frames():
 
 
 def parse_key(key):
-    recipe, size, spp, depth = key.split("_")
+    """'{recipe}_{W}x{H}_spp{n}_d{depth}[_whitted]' -> (recipe, W, H, spp, depth, whitted)"""
+    parts = key.split("_")
+    whitted = parts[-1] == "whitted"
+    recipe, size, spp, depth = parts[:4]
     W, H = map(int, size.split("x"))
-    return recipe, W, H, int(spp[3:]), int(depth[1:])
+    return recipe, W, H, int(spp[3:]), int(depth[1:]), whitted
 
 
 def test_oracle_reproduces_golden_hits(oracle, rt):
@@ -38,11 +41,13 @@ def test_oracle_reproduces_golden_hits(oracle, rt):
     assert np.array_equal(s.occluded(g["occl_rays"]), g["occluded"])
 
 
-@pytest.mark.parametrize("key", ["teapotF_320x180_spp1_d10", "cfg3_256x144_spp4_d4", "mig16_480x270_spp1_d1"])
+@pytest.mark.parametrize("key", ["teapotF_320x180_spp1_d10", "cfg3_256x144_spp4_d4", "mig16_480x270_spp1_d1",
+                                 "cfg3_256x144_spp1_d20_whitted", "teapotF_320x180_spp1_d20_whitted"])
 def test_oracle_reproduces_golden_frames(oracle, rt, key):
-    recipe, W, H, spp, depth = parse_key(key)
+    recipe, W, H, spp, depth, whitted = parse_key(key)
     want = frames()[key]
     s = oracle.Scene(recipe, rt.DATA_DIR)
+    s.set_integrator(int(whitted))
     acc = np.zeros((W * H, 4), np.float32)
     rgb, st = s.tick(W, H, acc, spp=spp, depth=depth, frame=0)
     assert zlib.crc32(rgb.astype("<u4").tobytes()) == want["rgb8_crc32"]
@@ -70,10 +75,11 @@ def test_gpu_matches_golden_frames(rt, key):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    recipe, W, H, spp, depth = parse_key(key)
+    recipe, W, H, spp, depth, whitted = parse_key(key)
     want = frames()[key]
     sc = rt.Scene.recipe(recipe)
     r = rt.Renderer(sc, W, H)
+    r.useWhitted = whitted
     rgb = r.tick_host(spp=spp, depth=depth, frame=0)
     c = r.counters()
     assert c["shadow"] == want["shadow"] and c["bounce"] == want["bounce"]

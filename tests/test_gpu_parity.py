@@ -97,8 +97,10 @@ def test_empty_batches(scenes, torch):
     assert g.IsOccluded(np.zeros((0, 7), np.float32)).numel() == 0
 
 
-def frame_vs_oracle(rt, g, o, W, H, spp, depth, frames=1, exact=True):
+def frame_vs_oracle(rt, g, o, W, H, spp, depth, frames=1, exact=True, whitted=False):
     r = rt.Renderer(g, W, H)
+    r.useWhitted = whitted
+    o.set_integrator(int(whitted))
     acc = np.zeros((W * H, 4), np.float32)
     total = {}
     for f in range(frames):
@@ -181,9 +183,36 @@ def test_sharded_frame_assembles_to_full_frame(rt, scenes, torch):
     assert np.array_equal(host, full.cpu().numpy())
 
 
-def test_textured_sky_and_planes(rt, oracle, torch):
-    """Non-constant power-of-two sky (renderer.h:15-22) and a plane primitive."""
+def twin_scene(rt, oracle, prims, mats, sky=None):
+    """The same hand-made scene in the product (device) and in the oracle."""
+    o = oracle_scene(rt, oracle, prims, mats, sky)
+    return rt.Scene(prims, mats, sky=sky), o
+
+
+def oracle_scene(rt, oracle, prims, mats, sky=None):
     import ctypes as C
+    L = oracle.lib()
+    h = L.or_scene_new()
+    f3 = lambda *v: (C.c_float * 3)(*v)
+    for m in mats:
+        L.or_scene_add_material(h, m.kind, f3(*m.color), f3(*m.color2), m.ior, m.diffuse)
+    for p in prims:
+        v = list(p.v)
+        if p.type == rt.SPHERE:
+            L.or_scene_add_sphere(h, f3(*v[:3]), v[3], p.material)
+        elif p.type == rt.PLANE:
+            L.or_scene_add_plane(h, f3(*v[:3]), v[3], p.material)
+        else:
+            L.or_scene_add_triangle(h, f3(*v[:3]), f3(*v[3:6]), f3(*v[6:9]), p.material)
+    if sky is not None:
+        L.or_scene_set_sky(h, sky.shape[1], sky.shape[0], sky.ctypes.data_as(C.POINTER(C.c_uint32)))
+    L.or_scene_build_bvh(h)
+    o = oracle.Scene.__new__(oracle.Scene)
+    o.L, o.h = L, h
+    return o
+
+
+def sky_scene(rt, oracle, make=twin_scene):
     rng = np.random.default_rng(5)
     sky = rng.integers(0, 1 << 24, size=(64, 128), dtype=np.uint32)
     mats = [rt.material(rt.LIGHT, (24, 24, 22)), rt.material(rt.DIFFUSE, (0.8, 0.3, 0.3)),
@@ -191,26 +220,66 @@ def test_textured_sky_and_planes(rt, oracle, torch):
             rt.material(rt.MIRROR, (0.9, 0.9, 0.9))]
     prims = [rt.sphere((0, 4, -2), 0.5, 0), rt.plane((0, 1, 0), 1.5, 2), rt.sphere((0.6, 0, 2.5), 0.7, 3),
              rt.triangle((-1, -1, 3), (1, -1, 3), (0, 1, 3), 1)]
-    g = rt.Scene(prims, mats, sky=sky)
-    # same scene in the oracle
-    L = oracle.lib()
-    h = L.or_scene_new()
-    fp = C.POINTER(C.c_float)
-    f3 = lambda *v: (C.c_float * 3)(*v)
-    for m in mats:
-        L.or_scene_add_material(h, m.kind, f3(*m.color), f3(*m.color2), m.ior, m.diffuse)
-    L.or_scene_add_sphere(h, f3(0, 4, -2), 0.5, 0)
-    L.or_scene_add_plane(h, f3(0, 1, 0), 1.5, 2)
-    L.or_scene_add_sphere(h, f3(0.6, 0, 2.5), 0.7, 3)
-    L.or_scene_add_triangle(h, f3(-1, -1, 3), f3(1, -1, 3), f3(0, 1, 3), 1)
-    L.or_scene_set_sky(h, 128, 64, sky.ctypes.data_as(C.POINTER(C.c_uint32)))
-    L.or_scene_build_bvh(h)
-    o = oracle.Scene.__new__(oracle.Scene)
-    o.L, o.h = L, h
+    return make(rt, oracle, prims, mats, sky)
+
+
+def glass_scene(rt, oracle, make=twin_scene):
+    """Two glass spheres in front of a mirror over a checkerboard: every Whitted branch
+    (Fresnel split, TIR, absorption inside, MIX checkerboard, mirror chains)."""
+    mats = [rt.material(rt.LIGHT, (24, 24, 22)), rt.material(rt.DIELECTRIC, (0.2, 0.05, 0.3), ior=1.5),
+            rt.material(rt.DIELECTRIC, (0.0, 0.0, 0.0), ior=2.4), rt.material(rt.MIRROR, (0.95, 0.9, 0.9)),
+            rt.material(rt.CHECKERBOARD, (0.1, 0.1, 0.1), (0.9, 0.9, 0.9), diffuse=0.6),
+            rt.material(rt.DIFFUSE, (0.2, 0.7, 0.3))]
+    prims = [rt.sphere((0, 4, -2), 0.5, 0), rt.sphere((-0.5, 0, 2), 0.6, 1), rt.sphere((0.7, -0.2, 2.6), 0.5, 2),
+             rt.plane((0, 1, 0), 1.0, 4), rt.triangle((-3, -1, 5), (3, -1, 5), (0, 3, 5), 3),
+             rt.triangle((-3, -1, -1.5), (0, 3, -1.5), (3, -1, -1.5), 3), rt.sphere((1.5, 0.5, 3.5), 0.4, 5)]
+    return make(rt, oracle, prims, mats)
+
+
+def test_textured_sky_and_planes(rt, oracle, torch):
+    """Non-constant power-of-two sky (renderer.h:15-22) and a plane primitive."""
+    g, o = sky_scene(rt, oracle)
     got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, 96, 64, 2, 5)
     assert np.abs(gacc - acc).max() <= PIX_TOL
     rays = random_rays(20000, 9)
     hits_equal(g.IntersectBVH(rays), o.intersect(rays))
+
+
+# ---- Renderer::WhittedTrace (renderer.cpp:138-195), the K-key integrator
+def whitted_check(rt, g, o, W, H, spp, depth, frames=1):
+    got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, W, H, spp, depth, frames=frames, whitted=True)
+    d = np.abs(gacc - acc)
+    assert d.max() <= PIX_TOL, d.max()
+    assert np.array_equal(got, want), f"{(got != want).sum()} RGB8 mismatches"
+    assert c["shadow"] == st["shadow"]
+    assert c["bounce"] == st["isect"] - W * H * spp * frames
+    return st
+
+
+def test_whitted_cfg3_depth20(rt, scenes):
+    g, o = scenes("cfg3")
+    whitted_check(rt, g, o, 256, 144, 1, 20)
+
+
+def test_whitted_teapot_textured_sky(rt, oracle, torch):
+    g, o = sky_scene(rt, oracle)
+    whitted_check(rt, g, o, 96, 64, 2, 20, frames=2)
+
+
+def test_whitted_glass_branching(rt, oracle, torch):
+    g, o = glass_scene(rt, oracle)
+    st = whitted_check(rt, g, o, 160, 120, 1, 20)
+    assert st["isect"] > 1.8 * 160 * 120   # the Fresnel split fans out
+
+
+def test_whitted_depth_limits(rt, oracle, torch):
+    g, o = glass_scene(rt, oracle)
+    for depth in (1, 2, 32):
+        whitted_check(rt, g, o, 64, 48, 1, depth)
+    r = rt.Renderer(g, 64, 48)
+    r.useWhitted = True
+    with pytest.raises(rt.RTError):
+        r.tick_host(depth=33)
 
 
 def test_prebuilt_bvh_path(rt, scenes):

@@ -26,7 +26,9 @@ SPHERE, PLANE, TRIANGLE = 0, 1, 4
 DIFFUSE, MIRROR, DIELECTRIC, CHECKERBOARD, LIGHT = 0, 1, 2, 3, 4
 MODE_PATH = 0
 MODE_WHITTED = 1
-DEFAULT_DEPTH = {MODE_PATH: 10, MODE_WHITTED: 20}   # renderer.h:9, renderer.h:13
+MODE_PACKET = 2
+# renderer.h:9, renderer.h:13, renderer.cpp:105 (TracePacket's bounces: Trace's default depth)
+DEFAULT_DEPTH = {MODE_PATH: 10, MODE_WHITTED: 20, MODE_PACKET: 10}
 RECIPES = ("teapotF", "teapot", "mig16", "cfg3", "cfg5")
 
 
@@ -118,6 +120,8 @@ def lib():
         "rt_occluded": ([vp, vp, vp, u32, vp], C.c_int),
         "rt_intersect_host": ([vp, vp, vp, u32], C.c_int),
         "rt_occluded_host": ([vp, vp, vp, u32], C.c_int),
+        "rt_intersect_packets": ([vp, vp, vp, u32, vp], C.c_int),
+        "rt_intersect_packets_host": ([vp, vp, vp, u32], C.c_int),
         "rt_camera_default": ([u32, u32, C.POINTER(Camera)], C.c_int),
         "rt_renderer_create": ([vp, u32, u32, C.POINTER(vp)], C.c_int),
         "rt_renderer_destroy": ([vp], C.c_int),
@@ -366,6 +370,18 @@ class Scene:
             _check(self.L.rt_intersect(self.h, C.c_void_p(r.data_ptr()), C.c_void_p(hits.data_ptr()), n, C.c_void_p(s)))
         return hits[:, 0], hits.view(torch.int32)[:, 1], hits[:, 2], hits[:, 3]
 
+    def IntersectBVHPacket(self, rays, stream=None):
+        """Batched Scene::IntersectBVHPacket: rays [64k, 64k+64) form packet k."""
+        torch = _torch()
+        r = _as_device_rays(rays, self.device)
+        n = r.shape[0]
+        hits = torch.empty((n, 4), dtype=torch.float32, device=r.device)
+        if n:
+            s = stream if stream is not None else torch.cuda.current_stream(r.device).cuda_stream
+            _check(self.L.rt_intersect_packets(self.h, C.c_void_p(r.data_ptr()), C.c_void_p(hits.data_ptr()), n,
+                                               C.c_void_p(s)))
+        return hits[:, 0], hits.view(torch.int32)[:, 1], hits[:, 2], hits[:, 3]
+
     def IsOccluded(self, rays, stream=None):
         """Batched Scene::IsOccluded: bool tensor."""
         torch = _torch()
@@ -383,6 +399,13 @@ class Scene:
         hits = np.zeros(len(rays), HIT_DTYPE)
         _check(self.L.rt_intersect_host(self.h, rays.ctypes.data_as(C.c_void_p), hits.ctypes.data_as(C.c_void_p),
                                         len(rays)))
+        return hits
+
+    def intersect_packets_host(self, rays):
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 7)
+        hits = np.zeros(len(rays), HIT_DTYPE)
+        _check(self.L.rt_intersect_packets_host(self.h, rays.ctypes.data_as(C.c_void_p),
+                                                hits.ctypes.data_as(C.c_void_p), len(rays)))
         return hits
 
     def occluded_host(self, rays):
@@ -404,11 +427,15 @@ class Renderer:
         self.h = C.c_void_p()
         _check(self.L.rt_renderer_create(scene.h, width, height, C.byref(self.h)))
         self.frame = 0
-        self.useWhitted = False   # renderer.h:158; toggled by the K key (renderer.h:138)
+        self.mode = MODE_PATH     # MODE_PATH / MODE_WHITTED / MODE_PACKET (the PACKET_TRAVERSAL build)
 
     @property
-    def mode(self):
-        return MODE_WHITTED if self.useWhitted else MODE_PATH
+    def useWhitted(self):       # renderer.h:158; toggled by the K key (renderer.h:138)
+        return self.mode == MODE_WHITTED
+
+    @useWhitted.setter
+    def useWhitted(self, on):
+        self.mode = MODE_WHITTED if on else MODE_PATH
 
     def close(self):
         h = getattr(self, "h", None)

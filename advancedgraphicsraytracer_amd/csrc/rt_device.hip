@@ -298,6 +298,55 @@ __device__ __forceinline__ bool occluded(const SceneView &S, const Trav<STRIDE> 
     return occluded_t<false>(S, T, r);
 }
 
+// ------------------------------------------------------------------ packet traversal (scene.h:322-412)
+// Scene::IntersectBVHPacket with the packet = the wave: lane l holds ray l of the 64-ray
+// packet.  The node, the stack and the "first active" ray are wave-uniform (node and
+// primitive loads are scalar, the stack lives in one VGPR: entry i in lane i); each lane
+// tests its own ray and a ballot finds the lowest hitting lane.  Inactive lanes (past the
+// end of the batch / off screen) never test and never lead.
+__device__ __forceinline__ float readlane_f(float v, uint32_t l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
+}
+
+template <bool FAST>
+__device__ __forceinline__ void packet_closest_hit_t(const SceneView &S, DRay &r, bool active) {
+    const uint32_t lane = __lane_id();
+    uint32_t fa = 0, ni = 0, sp = 0;
+    int stackv = 0;                                   // lane i: stack entry i (node index, depth < 64)
+    for (;;) {
+        ni = __builtin_amdgcn_readfirstlane(ni);
+        const float4 a = S.nodes[2 * ni], b = S.nodes[2 * ni + 1];
+        const uint32_t word = __float_as_uint(b.z), cnt = word & 0xffu, lf = word >> 8;
+        const uint64_t m = __ballot(active && slab_hit<FAST>(r, a, b));
+        uint32_t first = 0;                           // lanes >= first test a leaf
+        bool visit = true;
+        if (!((m >> fa) & 1u)) {
+            if (m == 0) visit = false;
+            else first = fa = (uint32_t)__ffsll((long long)m) - 1u;
+        }
+        if (visit && cnt == 0) {                      // interior: order by the leader's distances
+            const float4 *q = S.nodes + 2 * lf;
+            float d1 = readlane_f(slab_dist<FAST>(r, q[0], q[1]), fa);
+            float d2 = readlane_f(slab_dist<FAST>(r, q[2], q[3]), fa);
+            uint32_t c1 = lf, c2 = lf + 1;
+            if (d1 > d2) { c1 = lf + 1; c2 = lf; }
+            stackv = lane == sp ? (int)c2 : stackv;   // writelane
+            ++sp;
+            ni = c1;
+            continue;
+        }
+        if (visit && active && lane >= first)
+            for (uint32_t k = lf; k < lf + cnt; ++k) prim_intersect(S, k, r);
+        if (sp == 0) break;
+        --sp;
+        ni = (uint32_t)__builtin_amdgcn_readlane(stackv, (int)sp);
+    }
+}
+__device__ __forceinline__ void packet_closest_hit(const SceneView &S, DRay &r, bool active) {
+    if (__all(S.bounds_finite && (!active || ray_finite(r)))) packet_closest_hit_t<true>(S, r, active);
+    else packet_closest_hit_t<false>(S, r, active);
+}
+
 // ------------------------------------------------------------------ shading
 // TEX_SKY = false: every texel is equal (the synthetic sky), so the lookup's index is
 // irrelevant and the colour is the precomputed texel -- bit-identical, no atan2/acos.
@@ -450,13 +499,12 @@ __device__ __forceinline__ f3 nee(const SceneView &S, const Trav<STRIDE> &T, f3 
 // so the float evaluation order is the reference's.
 template <int MAXD, bool TEX_SKY, int STRIDE>
 __device__ f3 trace_path(const SceneView &S, const Trav<STRIDE> &T, DRay ray, int depth, uint32_t &seed,
-                         uint32_t &nshadow, uint32_t &nbounce) {
+                         uint32_t &nshadow, uint32_t &nbounce, bool lastSpec = true) {
     f3 lv_mul[MAXD], lv_add[MAXD];
     float lv_c[MAXD];
     bool lv_diff[MAXD];
     int levels = 0;
     f3 term = mk(0, 0, 0);
-    bool lastSpec = true;
     for (int d = depth; d > 0 && levels < MAXD; --d) {
         if (d != depth) ++nbounce;
         closest_hit(S, T, ray);
@@ -493,6 +541,38 @@ __device__ f3 trace_path(const SceneView &S, const Trav<STRIDE> &T, DRay ray, in
     for (int k = levels - 1; k >= 0; --k)
         r = lv_diff[k] ? lv_mul[k] * ((r * lv_c[k]) / kINV2PI) + lv_add[k] : lv_mul[k] * r;
     return r;
+}
+
+// Renderer::TracePacket's per-ray shading (renderer.cpp:78-133): the primary hit comes
+// from the packet traversal, every bounce is a Trace(ray_out, specularBounce, depth).
+template <int MAXD, bool TEX_SKY, int STRIDE>
+__device__ f3 shade_packet(const SceneView &S, const Trav<STRIDE> &T, const DRay &ray, int depth, uint32_t &seed,
+                           uint32_t &nshadow, uint32_t &nbounce) {
+    if (ray.obj == -1) return sky_color<TEX_SKY>(S, ray.D);
+    f3 I = ray.O + ray.t * ray.D;
+    float4 s0 = S.shade[2 * ray.obj], s1 = S.shade[2 * ray.obj + 1];
+    f3 N = __float_as_uint(s1.x) == T_SPH ? (I - mk(s0.x, s0.y, s0.z)) * s1.y : mk(s0.x, s0.y, s0.z);
+    if (dot(N, ray.D) > 0) N = -N;                                     // Scene::GetNormal
+    const DevMaterial &m = S.mats[__float_as_int(s0.w)];
+    const bool last = depth == 0;                  // Trace(.., 0) returns 0: the bounce is never traced
+    DRay out;
+    bool spec = scatter(m, ray, I, N, out, seed, last);
+    f3 albedo = mat_color(m, ray, I);
+    if (m.flag == F_LIGHT) return albedo;
+    const bool diffuse = m.flag == F_DIFFUSE || m.flag == F_MIX;
+    // MIX + specular bounce: the ray is traced for a result that is then overwritten
+    // (renderer.cpp:111-114) and traced again after NEE (116-120).  One call site.
+    const int passes = (m.flag == F_MIX && spec) ? 2 : 1;
+    const f3 BRDF = albedo * kINVPI;
+    f3 Ld = mk(0, 0, 0), Li = mk(0, 0, 0);
+    for (int p = 0; p < passes; ++p) {
+        if (diffuse && p == passes - 1) Ld = nee(S, T, I, N, BRDF, seed, nshadow);
+        nbounce += last ? 0u : 1u;
+        Li = trace_path<MAXD, TEX_SKY>(S, T, out, depth, seed, nshadow, nbounce, spec);
+    }
+    if (!diffuse) return albedo * Li;
+    f3 Ei = (Li * (last ? 0.0f : dot(N, out.D))) / kINV2PI;
+    return BRDF * Ei + Ld;
 }
 
 // ------------------------------------------------------------------ Whitted (the K key)
@@ -691,23 +771,36 @@ __device__ __forceinline__ uint32_t pack_rgb8(float4 a) {
 }
 
 // ------------------------------------------------------------------ kernels
-// One screen tile (8x8, one wave) of one frame: per pixel spp x Trace (MAXD = 0: WhittedTrace), running average
-// into the accumulator (renderer.cpp:235-241), RGB8 pack; per-wave ray counters.
-template <int MAXD, bool TEX_SKY, int STRIDE>
+// One screen tile (8x8, one wave) of one frame: per pixel spp x Trace / WhittedTrace /
+// TracePacket (the tile is the packet, renderer.cpp:247-285), running average into the
+// accumulator (renderer.cpp:235-241), RGB8 pack; per-wave ray counters.
+enum : int { M_PATH = RT_MODE_PATH, M_WHITTED = RT_MODE_WHITTED, M_PACKET = RT_MODE_PACKET };
+
+template <int MODE, int MAXD, bool TEX_SKY, int STRIDE>
 __device__ __forceinline__ void render_tile(const SceneView &S, const FrameArgs &F, const Trav<STRIDE> &T,
                                             uint32_t local_tile, uint32_t lane) {
     const uint32_t tile = local_tile * F.nshards + F.shard;
     const uint32_t x = (tile % F.tiles_x) * 8u + (lane & 7u), y = (tile / F.tiles_x) * 8u + (lane >> 3);
+    const bool on = x < F.W && y < F.H;
+    const uint32_t px = x + y * F.W;
     uint32_t nshadow = 0, nbounce = 0;
-    if (x < F.W && y < F.H) {
-        const uint32_t px = x + y * F.W;
-        f3 sum = mk(0, 0, 0);
+    f3 sum = mk(0, 0, 0);
+    if (MODE == M_PACKET) {                           // the traversal is wave-wide: no early exit
+        for (uint32_t s = 0; s < F.spp; ++s) {
+            uint32_t seed = init_seed(px + F.W * F.H * (s + F.spp * F.frame));
+            DRay ray = on ? primary_ray(F, x, y, seed) : make_ray(mk(0, 0, 0), mk(0, 0, 1), 1e34f);
+            packet_closest_hit(S, ray, on);
+            if (on) sum = sum + shade_packet<MAXD, TEX_SKY>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
+        }
+    } else if (on) {
         for (uint32_t s = 0; s < F.spp; ++s) {
             uint32_t seed = init_seed(px + F.W * F.H * (s + F.spp * F.frame));
             DRay ray = primary_ray(F, x, y, seed);
-            if constexpr (MAXD == 0) sum = sum + trace_whitted<TEX_SKY>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
+            if constexpr (MODE == M_WHITTED) sum = sum + trace_whitted<TEX_SKY>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
             else sum = sum + trace_path<MAXD, TEX_SKY>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
         }
+    }
+    if (on) {
         f3 res = (1.0f / (float)F.spp) * sum;
         float4 a = F.reset ? make_float4(0, 0, 0, 0) : F.acc[px];
         a.w += 1;                                                      // renderer.cpp:237-240
@@ -731,14 +824,14 @@ __device__ __forceinline__ void render_tile(const SceneView &S, const FrameArgs 
 #ifndef RT_RENDER_WAVES_PER_SIMD
 #define RT_RENDER_WAVES_PER_SIMD 1
 #endif
-template <int MAXD, bool TEX_SKY>
+template <int MODE, int MAXD, bool TEX_SKY>
 __global__ __launch_bounds__(256, RT_RENDER_WAVES_PER_SIMD) void k_render(SceneView S, FrameArgs F) {
     extern __shared__ uint32_t lds_stack[];
     const uint32_t tid = threadIdx.x;
     const uint32_t local_tile = blockIdx.x * 4u + (tid >> 6);
     if (local_tile >= F.ntiles_local) return;
     Trav<256> T{S.nodes, lds_stack + tid};
-    render_tile<MAXD, TEX_SKY>(S, F, T, local_tile, tid & 63u);
+    render_tile<MODE, MAXD, TEX_SKY>(S, F, T, local_tile, tid & 63u);
 }
 
 // LDS-node variant for scenes whose node array fits beside the stacks (TEAPOT-F: 65 KB):
@@ -757,7 +850,7 @@ __global__ __launch_bounds__(1024) void k_render_lds(SceneView S, FrameArgs F) {
     const uint32_t local_tile = blockIdx.x * 16u + (tid >> 6);
     if (local_tile >= F.ntiles_local) return;
     Trav<1024> T{lnodes, lds + tid};
-    render_tile<MAXD, TEX_SKY>(S, F, T, local_tile, tid & 63u);
+    render_tile<M_PATH, MAXD, TEX_SKY>(S, F, T, local_tile, tid & 63u);
 }
 
 __global__ __launch_bounds__(256) void k_intersect(SceneView S, const rt_ray *__restrict__ rays, rt_hit *__restrict__ hits,
@@ -769,6 +862,25 @@ __global__ __launch_bounds__(256) void k_intersect(SceneView S, const rt_ray *__
     DRay r = make_ray(mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), q.tmax);
     Trav<256> T{S.nodes, lds_stack + threadIdx.x};
     closest_hit(S, T, r);
+    finish_uv(S, r);
+    rt_hit h;
+    h.t = r.t; h.obj = r.obj; h.u = r.u; h.v = r.v;
+    hits[i] = h;
+}
+
+// batched Scene::IntersectBVHPacket: wave w traces rays [64w, 64w + 64) as one packet
+__global__ __launch_bounds__(256) void k_intersect_packet(SceneView S, const rt_ray *__restrict__ rays,
+                                                          rt_hit *__restrict__ hits, uint32_t n) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if ((i & ~63u) >= n) return;                      // whole waves only
+    const bool active = i < n;
+    DRay r = make_ray(mk(0, 0, 0), mk(0, 0, 1), 1e34f);
+    if (active) {
+        rt_ray q = rays[i];
+        r = make_ray(mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), q.tmax);
+    }
+    packet_closest_hit(S, r, active);
+    if (!active) return;
     finish_uv(S, r);
     rt_hit h;
     h.t = r.t; h.obj = r.obj; h.u = r.u; h.v = r.v;
@@ -1121,7 +1233,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     if (p->width != r->W || p->height != r->H)
         return fail(RT_ERR_INVALID, "frame size differs from the renderer's accumulator");
     if (p->spp == 0) return fail(RT_ERR_INVALID, "spp must be >= 1");
-    if (p->mode != RT_MODE_PATH && p->mode != RT_MODE_WHITTED) return fail(RT_ERR_INVALID, "unknown integrator mode");
+    if (p->mode > RT_MODE_PACKET) return fail(RT_ERR_INVALID, "unknown integrator mode");
     if (nshards == 0 || shard >= nshards) return fail(RT_ERR_INVALID, "bad shard index");
     rt_scene *s = r->scene;
     HIP_TRY(hipSetDevice(s->device));
@@ -1145,12 +1257,13 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     hipStream_t st = (hipStream_t)stream;
     const uint32_t depth = p->depth;
     if (depth > 32) return fail(RT_ERR_UNSUPPORTED, "Trace depth above 32");   // = kWHITTED_MAX
-    const int md = p->mode == RT_MODE_WHITTED ? 0 : depth <= 1 ? 1 : depth <= 4 ? 4 : depth <= 10 ? 10 : 32;
+    const int md = depth <= 1 ? 1 : depth <= 4 ? 4 : depth <= 10 ? 10 : 32;
     const bool tex = !s->view.sky_const;
+    const int mode = (int)p->mode;
     // LDS nodes pay off where registers allow 1024-thread workgroups without spilling:
     // the primary+shadow kernel with the constant sky (103 VGPRs); the path-tracing
     // variants keep the 256-thread global-node kernel (A/B in profiles/r01).
-    const bool use_lds = s->lds_nodes && md == 1 && !tex;
+    const bool use_lds = s->lds_nodes && mode == RT_MODE_PATH && md == 1 && !tex;
     dim3 grid, block;
     size_t lds;
     if (use_lds) {
@@ -1162,19 +1275,29 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         block = dim3(256);
         lds = stack_bytes(s);
     }
-#define RT_LAUNCH(MD, TX) hipLaunchKernelGGL((k_render<MD, TX>), grid, block, lds, st, s->view, F)
+#define RT_LAUNCH(MO, MD, TX) hipLaunchKernelGGL((k_render<MO, MD, TX>), grid, block, lds, st, s->view, F)
     if (use_lds) hipLaunchKernelGGL((k_render_lds<1, false>), grid, block, lds, st, s->view, F);
-    else switch (md * 2 + (tex ? 1 : 0)) {
-    case 0: RT_LAUNCH(0, false); break;
-    case 1: RT_LAUNCH(0, true); break;
-    case 2: RT_LAUNCH(1, false); break;
-    case 3: RT_LAUNCH(1, true); break;
-    case 8: RT_LAUNCH(4, false); break;
-    case 9: RT_LAUNCH(4, true); break;
-    case 20: RT_LAUNCH(10, false); break;
-    case 21: RT_LAUNCH(10, true); break;
-    case 64: RT_LAUNCH(32, false); break;
-    default: RT_LAUNCH(32, true); break;
+    else if (mode == RT_MODE_WHITTED) {
+        if (tex) RT_LAUNCH(M_WHITTED, 1, true); else RT_LAUNCH(M_WHITTED, 1, false);
+    } else if (mode == RT_MODE_PACKET) {                // depth = the bounces' Trace depth (0 allowed)
+        const int pd = depth <= 1 ? 1 : depth <= 10 ? 10 : 32;
+        switch (pd * 2 + (tex ? 1 : 0)) {
+        case 2: RT_LAUNCH(M_PACKET, 1, false); break;
+        case 3: RT_LAUNCH(M_PACKET, 1, true); break;
+        case 20: RT_LAUNCH(M_PACKET, 10, false); break;
+        case 21: RT_LAUNCH(M_PACKET, 10, true); break;
+        case 64: RT_LAUNCH(M_PACKET, 32, false); break;
+        default: RT_LAUNCH(M_PACKET, 32, true); break;
+        }
+    } else switch (md * 2 + (tex ? 1 : 0)) {
+    case 2: RT_LAUNCH(M_PATH, 1, false); break;
+    case 3: RT_LAUNCH(M_PATH, 1, true); break;
+    case 8: RT_LAUNCH(M_PATH, 4, false); break;
+    case 9: RT_LAUNCH(M_PATH, 4, true); break;
+    case 20: RT_LAUNCH(M_PATH, 10, false); break;
+    case 21: RT_LAUNCH(M_PATH, 10, true); break;
+    case 64: RT_LAUNCH(M_PATH, 32, false); break;
+    default: RT_LAUNCH(M_PATH, 32, true); break;
     }
 #undef RT_LAUNCH
     HIP_TRY(hipGetLastError());
@@ -1274,7 +1397,17 @@ int rt_occluded(rt_scene *s, const rt_ray *rays, uint8_t *out, uint32_t n, void 
     return RT_OK;
 }
 
-static int staged_call(rt_scene *s, const rt_ray *rays, void *out, size_t out_elem, uint32_t n, bool occl) {
+int rt_intersect_packets(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t n, void *stream) {
+    if (!s || (n && (!rays || !hits))) return fail(RT_ERR_INVALID, "rt_intersect_packets: null argument");
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_intersect_packet, dim3((n + 255) / 256), dim3(256), 0, st, s->view, rays, hits, n);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+enum { CALL_INTERSECT, CALL_OCCLUDED, CALL_PACKETS };
+static int staged_call(rt_scene *s, const rt_ray *rays, void *out, size_t out_elem, uint32_t n, int kind) {
     if (!s || (n && (!rays || !out))) return fail(RT_ERR_INVALID, "null argument");
     if (n == 0) return RT_OK;
     HIP_TRY(hipSetDevice(s->device));
@@ -1289,7 +1422,9 @@ static int staged_call(rt_scene *s, const rt_ray *rays, void *out, size_t out_el
     rt_ray *d_rays = (rt_ray *)s->d_scratch;
     char *d_out = (char *)s->d_scratch + (((size_t)n * sizeof(rt_ray) + 255) & ~(size_t)255);
     HIP_TRY(hipMemcpyAsync(d_rays, rays, sizeof(rt_ray) * n, hipMemcpyHostToDevice, s->stream));
-    int rc = occl ? rt_occluded(s, d_rays, (uint8_t *)d_out, n, s->stream) : rt_intersect(s, d_rays, (rt_hit *)d_out, n, s->stream);
+    int rc = kind == CALL_OCCLUDED ? rt_occluded(s, d_rays, (uint8_t *)d_out, n, s->stream)
+             : kind == CALL_PACKETS ? rt_intersect_packets(s, d_rays, (rt_hit *)d_out, n, s->stream)
+                                    : rt_intersect(s, d_rays, (rt_hit *)d_out, n, s->stream);
     if (rc != RT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(out, d_out, out_elem * n, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -1297,10 +1432,13 @@ static int staged_call(rt_scene *s, const rt_ray *rays, void *out, size_t out_el
 }
 
 int rt_intersect_host(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t n) {
-    return staged_call(s, rays, hits, sizeof(rt_hit), n, false);
+    return staged_call(s, rays, hits, sizeof(rt_hit), n, CALL_INTERSECT);
 }
 int rt_occluded_host(rt_scene *s, const rt_ray *rays, uint8_t *out, uint32_t n) {
-    return staged_call(s, rays, out, 1, n, true);
+    return staged_call(s, rays, out, 1, n, CALL_OCCLUDED);
+}
+int rt_intersect_packets_host(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t n) {
+    return staged_call(s, rays, hits, sizeof(rt_hit), n, CALL_PACKETS);
 }
 
 int rt_renderer_create(rt_scene *s, uint32_t W, uint32_t H, rt_renderer **out) {

@@ -49,9 +49,12 @@ enum { RT_SPHERE = 0, RT_PLANE = 1, RT_TRIANGLE = 4 };
 /* Materials: Diffuse.h, Mirror.h, Dielectric.h, Checkerboard.h, Light.h. */
 enum { RT_DIFFUSE = 0, RT_MIRROR = 1, RT_DIELECTRIC = 2, RT_CHECKERBOARD = 3, RT_LIGHT = 4 };
 /* Integrators behind Renderer::Tick (renderer.cpp:227-231; the K key toggles them,
- * renderer.h:138): Trace (path tracer, default depth 10, renderer.h:9) and WhittedTrace
- * (default depth 20, renderer.h:13).  depth <= 32 for both. */
-enum { RT_MODE_PATH = 0, RT_MODE_WHITTED = 1 };
+ * renderer.h:138): Trace (path tracer, default depth 10, renderer.h:9), WhittedTrace
+ * (default depth 20, renderer.h:13), and the PACKET_TRAVERSAL build of Tick
+ * (renderer.cpp:247-285): 8x8 tiles as 64-ray packets through IntersectBVHPacket, shaded
+ * by TracePacket whose bounces are Trace(.., depth) -- depth 10 in the reference, 0 allowed.
+ * depth <= 32 for all three. */
+enum { RT_MODE_PATH = 0, RT_MODE_WHITTED = 1, RT_MODE_PACKET = 2 };
 
 /* One primitive, Primitive::create* factories (Primitive.h:690-747):
  *   RT_SPHERE:   v[0..2] centre, v[3] radius
@@ -141,9 +144,14 @@ int rt_scene_copy_bvh(const rt_scene *s, void *nodes, uint32_t *indices);
 int rt_intersect(rt_scene *s, const rt_ray *rays_dev, rt_hit *hits_dev, uint32_t n, void *stream);
 /* Batched Scene::IsOccluded (template/scene.h:452-487): out_dev[i] = 1 if occluded. */
 int rt_occluded(rt_scene *s, const rt_ray *rays_dev, uint8_t *out_dev, uint32_t n, void *stream);
-/* Host-pointer conveniences of the two above (copy in, launch, copy out, sync). */
+/* Batched Scene::IntersectBVHPacket (template/scene.h:322-412, RayPacket Ray.h:34-64):
+ * rays [64k, 64k + 64) form packet k (PACKET_SIZE 64) and share one first-active
+ * traversal; the last packet may be partial (its missing slots take no part). */
+int rt_intersect_packets(rt_scene *s, const rt_ray *rays_dev, rt_hit *hits_dev, uint32_t n, void *stream);
+/* Host-pointer conveniences of the three above (copy in, launch, copy out, sync). */
 int rt_intersect_host(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t n);
 int rt_occluded_host(rt_scene *s, const rt_ray *rays, uint8_t *out, uint32_t n);
+int rt_intersect_packets_host(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t n);
 
 /* ---- renderer (Renderer, renderer.h:5-160) -------------------------------- */
 /* Camera::Camera (camera.h:28-41) for a W x H target */

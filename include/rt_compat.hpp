@@ -6,6 +6,7 @@
 //   Tmpl8::Ray                 Ray.h:7-32 (O, D, rD, t, objIdx, inside, u, v)
 //   Tmpl8::Scene::IntersectBVH template/scene.h:285   -> rt_intersect_host (batch of 1 or n)
 //   Tmpl8::Scene::IsOccluded   template/scene.h:452   -> rt_occluded_host
+//   Tmpl8::Scene::IntersectBVHPacket template/scene.h:322 -> rt_intersect_packets_host
 //   Tmpl8::Camera              camera.h:28-52         -> rt_camera_default
 //   Tmpl8::Renderer::Tick      renderer.cpp:200-309   -> rt_render_frame_host
 //
@@ -44,6 +45,18 @@ class Ray {   // Ray.h:7-32
     float u = 0, v = 0;
 };
 
+constexpr int PACKET_SIZE = 64;   // Ray.h:4
+
+struct RayPacket {   // Ray.h:34-64 (SoA, one 8x8 tile of primary rays)
+    float3 O[PACKET_SIZE], D[PACKET_SIZE];
+    float t[PACKET_SIZE], u[PACKET_SIZE] = {}, v[PACKET_SIZE] = {};
+    int objIdx[PACKET_SIZE];
+    int firstActive = 0;
+    RayPacket() {
+        for (int i = 0; i < PACKET_SIZE; ++i) t[i] = 1e34f, objIdx[i] = -1;
+    }
+};
+
 class Scene {   // template/scene.h:37
   public:
     explicit Scene(const char *recipe, const char *mesh_dir, int device = 0) {
@@ -62,11 +75,30 @@ class Scene {   // template/scene.h:37
         std::vector<rt_hit> out(in.size());
         rt_check(rt_intersect_host(h_, in.data(), out.data(), (uint32_t)in.size()));
         for (size_t i = 0; i < rays.size(); ++i) {
+            if (out[i].obj < 0) continue;   // nothing closer than ray.t: the ray is left as it was
             rays[i]->t = out[i].t;
             rays[i]->objIdx = out[i].obj;
             rays[i]->u = out[i].u;
             rays[i]->v = out[i].v;
         }
+    }
+    // Scene::IntersectBVHPacket (template/scene.h:322-412) on one or more packets
+    void IntersectBVHPacket(RayPacket &p) { IntersectBVHPacket(&p, 1); }
+    void IntersectBVHPacket(RayPacket *packets, size_t count) {
+        std::vector<rt_ray> in(count * PACKET_SIZE);
+        for (size_t k = 0; k < count; ++k)
+            for (int i = 0; i < PACKET_SIZE; ++i) {
+                const RayPacket &p = packets[k];
+                in[k * PACKET_SIZE + i] = rt_ray{p.O[i].x, p.O[i].y, p.O[i].z, p.D[i].x, p.D[i].y, p.D[i].z, p.t[i]};
+            }
+        std::vector<rt_hit> out(in.size());
+        rt_check(rt_intersect_packets_host(h_, in.data(), out.data(), (uint32_t)in.size()));
+        for (size_t k = 0; k < count; ++k)
+            for (int i = 0; i < PACKET_SIZE; ++i) {
+                const rt_hit &h = out[k * PACKET_SIZE + i];
+                if (h.obj < 0) continue;
+                packets[k].t[i] = h.t; packets[k].objIdx[i] = h.obj; packets[k].u[i] = h.u; packets[k].v[i] = h.v;
+            }
     }
     std::vector<bool> IsOccluded(std::vector<Ray *> &rays) {
         std::vector<rt_ray> in = pack(rays);
@@ -107,10 +139,11 @@ class Renderer {   // renderer.h:5-160
 
     // One frame: Trace (depth 10, renderer.h:9) or WhittedTrace (depth 20, renderer.h:13)
     // per pixel, accumulate, pack into pixels.  depth 0 = the reference's default.
+    // usePackets = the PACKET_TRAVERSAL build (Ray.h:3): 8x8 packets through TracePacket.
     void Tick(float /*deltaTime*/, uint32_t depth = 0, uint32_t spp = 1) {
         if (depth == 0) depth = useWhitted ? 20 : 10;
-        rt_frame_params p{width_, height_, spp, depth, frame_++, useWhitted ? RT_MODE_WHITTED : RT_MODE_PATH,
-                          swapped_ ? 1u : 0u};
+        const uint32_t mode = useWhitted ? RT_MODE_WHITTED : usePackets ? RT_MODE_PACKET : RT_MODE_PATH;
+        rt_frame_params p{width_, height_, spp, depth, frame_++, mode, swapped_ ? 1u : 0u};
         swapped_ = false;
         rt_check(rt_render_frame_host(h_, &camera.cam, &p, pixels.data()));
     }
@@ -129,6 +162,7 @@ class Renderer {   // renderer.h:5-160
 
   public:
     bool useWhitted = false;        // renderer.h:158
+    bool usePackets = false;        // PACKET_TRAVERSAL, Ray.h:3
     std::vector<uint32_t> pixels;   // 0x00RRGGBB, the reference's screen->pixels
 };
 

@@ -71,6 +71,7 @@ def lib():
                               fp, C.POINTER(C.c_uint32), C.POINTER(Stats), C.c_int]
         L.or_camera_rays.argtypes = [C.POINTER(Camera), C.c_int, C.c_int, C.c_int, ip, C.c_int, fp]
         L.or_intersect.argtypes = [vp, fp, C.c_int, fp, ip, fp, fp, C.c_int]
+        L.or_intersect_packets.argtypes = [vp, fp, C.c_int, fp, ip, fp, fp]
         L.or_occluded.argtypes = [vp, fp, C.c_int, C.POINTER(C.c_uint8)]
         L.or_obj_parse.argtypes = [C.c_char_p, C.POINTER(fp), ip, C.POINTER(ip), ip]
         L.or_obj_parse.restype = C.c_int
@@ -114,7 +115,7 @@ class Scene:
             self.h = None
 
     def set_integrator(self, mode):
-        """0 = Renderer::Trace (path tracer), 1 = Renderer::WhittedTrace."""
+        """0 = Renderer::Trace (path tracer), 1 = Renderer::WhittedTrace, 2 = packet mode."""
         self.L.or_scene_set_integrator(self.h, mode)
 
     @property
@@ -190,6 +191,15 @@ class Scene:
         t = np.empty(n, np.float32); o = np.empty(n, np.int32); u = np.empty(n, np.float32); v = np.empty(n, np.float32)
         self.L.or_intersect(self.h, _p(rays, C.c_float), n, _p(t, C.c_float), _p(o, C.c_int32), _p(u, C.c_float),
                             _p(v, C.c_float), int(brute))
+        return t, o, u, v
+
+    def intersect_packets(self, rays):
+        """Scene::IntersectBVHPacket over packets of 64 consecutive rays."""
+        rays = np.ascontiguousarray(rays, dtype=np.float32)
+        n = len(rays)
+        t = np.empty(n, np.float32); o = np.empty(n, np.int32); u = np.empty(n, np.float32); v = np.empty(n, np.float32)
+        self.L.or_intersect_packets(self.h, _p(rays, C.c_float), n, _p(t, C.c_float), _p(o, C.c_int32),
+                                    _p(u, C.c_float), _p(v, C.c_float))
         return t, o, u, v
 
     def occluded(self, rays):

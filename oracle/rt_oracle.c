@@ -913,10 +913,115 @@ static f3 whitted(const or_scene *s, ray_t *ray, int depth, uint32_t *seed, coun
     return mul(mk(cv[0], cv[1], cv[2]), result);
 }
 
+/* Scene::IntersectBVHPacket, template/scene.h:322-412: 64 rays share one traversal led by
+ * the "first active" ray.  The reference fills off-screen slots of edge packets with
+ * uninitialised rays; here they are inactive (never tested, never lead). */
+static void intersect_packet(const or_scene *s, ray_t *R, const int *active, counters *k) {
+    int fa = 0;                                  /* slot 0 is always on screen */
+    const node *n = &s->nodes[0];
+    const node *stack[64];
+    uint32_t sp = 0;
+    if (k) for (int i = 0; i < 64; i++) k->isect += active[i];
+    for (;;) {
+        if (hits_aabb(&R[fa], n)) {
+            if (n->count > 0) {
+                for (int i = 0; i < 64; i++) {
+                    if (!active[i]) continue;
+                    for (uint32_t j = 0; j < n->count; j++) {
+                        int oi = (int)s->idx[n->leftFirst + j];
+                        prim_intersect(&s->p[oi], &R[i], oi);
+                    }
+                }
+                if (sp == 0) break;
+                n = stack[--sp];
+                continue;
+            }
+        } else {
+            int found = -1;
+            for (int i = 0; i < 64; i++)
+                if (active[i] && hits_aabb(&R[i], n)) { found = i; break; }
+            if (found < 0) {
+                if (sp == 0) break;
+                n = stack[--sp];
+                continue;
+            }
+            fa = found;
+            if (n->count > 0) {
+                for (int i = fa; i < 64; i++) {
+                    if (!active[i]) continue;
+                    for (uint32_t j = 0; j < n->count; j++) {
+                        int oi = (int)s->idx[n->leftFirst + j];
+                        prim_intersect(&s->p[oi], &R[i], oi);
+                    }
+                }
+                if (sp == 0) break;
+                n = stack[--sp];
+                continue;
+            }
+        }
+        const node *c1 = &s->nodes[n->leftFirst], *c2 = &s->nodes[n->leftFirst + 1];
+        float d1 = intersect_aabb(&R[fa], c1), d2 = intersect_aabb(&R[fa], c2);
+        if (d1 > d2) { float td = d1; d1 = d2; d2 = td; const node *tn = c1; c1 = c2; c2 = tn; }
+        n = c1;
+        if (sp == 64) { fprintf(stderr, "oracle: packet stack overflow\n"); abort(); }
+        stack[sp++] = c2;
+    }
+}
+
+/* Renderer::TracePacket's per-ray shading, renderer.cpp:78-133 (bounces: Trace, depth given) */
+static f3 shade_packet_ray(const or_scene *s, ray_t *ray, int depth, uint32_t *seed, counters *k) {
+    if (ray->obj == -1) return sky_color(s, ray->D);
+    f3 I = add(ray->O, smul(ray->t, ray->D));
+    f3 N = scene_normal(s, ray->obj, I, ray->D);
+    const material *m = &s->m[s->p[ray->obj].mat];
+    ray_t out = mkray(mk(0, 0, 0), mk(1, 1, 1), 1e34f);
+    int spec = mat_scatter(m, ray, I, N, &out, seed);
+    f3 albedo = mat_color(m, ray);
+    int flag = mat_flag(m);
+    if (flag == FLAG_DIFFUSE || flag == FLAG_MIX) {
+        /* MIX: a specular bounce is traced once for a result that is then overwritten
+         * (renderer.cpp:111-114), and the same ray is traced again below (116-120) */
+        if (flag == FLAG_MIX && spec) (void)trace(s, &out, spec, depth, seed, k);
+        f3 BRDF = muls(albedo, INVPI_F);
+        float PDF = INV2PI_F;
+        f3 Ld = nee(s, I, N, BRDF, seed, k);
+        f3 Ei = divs(muls(trace(s, &out, spec, depth, seed, k), dot(N, out.D)), PDF);
+        return add(mul(BRDF, Ei), Ld);
+    } else if (flag == FLAG_SPECULAR || flag == FLAG_DIELECTRIC) {
+        return mul(albedo, trace(s, &out, spec, depth, seed, k));
+    }
+    return albedo;   /* LIGHT */
+}
+
+static uint32_t pixel_seed(int W, int H, int pixel, int sample, int spp, int frame);
+
+/* One 8x8 packet tile (the PACKET_TRAVERSAL branch of Renderer::Tick, renderer.cpp:247-285),
+ * averaged over spp packets; out[lane] for lane = xp + 8 * yp. */
+static void packet_tile(const or_scene *s, const or_camera *c, int W, int H, int spp, int depth, int frame,
+                        int tx, int ty, f3 *out, counters *k) {
+    ray_t R[64];
+    uint32_t seed[64];
+    int active[64];
+    for (int l = 0; l < 64; l++) out[l] = mk(0, 0, 0);
+    for (int smp = 0; smp < spp; smp++) {
+        for (int l = 0; l < 64; l++) {
+            int x = tx * 8 + (l & 7), y = ty * 8 + (l >> 3);
+            active[l] = x < W && y < H;
+            if (!active[l]) continue;
+            seed[l] = pixel_seed(W, H, x + y * W, smp, spp, frame);
+            R[l] = primary_ray(c, x, y, &seed[l]);
+        }
+        intersect_packet(s, R, active, k);
+        for (int l = 0; l < 64; l++)
+            if (active[l]) out[l] = add(out[l], shade_packet_ray(s, &R[l], depth, &seed[l], k));
+    }
+    for (int l = 0; l < 64; l++) out[l] = smul(1.0f / (float)spp, out[l]);
+}
+
 void or_scene_set_integrator(or_scene *s, int mode) { s->integrator = mode; }
 
 /* ------------------------------------------------------------------ drivers */
-static inline uint32_t pixel_seed(int W, int H, int pixel, int sample, int spp, int frame) {
+static uint32_t pixel_seed(int W, int H, int pixel, int sample, int spp, int frame) {
     return or_init_seed((uint32_t)pixel + (uint32_t)W * (uint32_t)H * (uint32_t)(sample + spp * frame));
 }
 
@@ -964,10 +1069,15 @@ static f3 trace_pixel(const or_scene *s, const or_camera *c, int W, int H, int s
                       int px, counters *k) {
     f3 res = mk(0, 0, 0);
     int x = px % W, y = px / W;
+    if (s->integrator == 2) {   /* the pixel's whole packet is traced; its counters are not kept */
+        f3 tile[64];
+        packet_tile(s, c, W, H, spp, depth, frame, x / 8, y / 8, tile, NULL);
+        return tile[(x & 7) + 8 * (y & 7)];
+    }
     for (int smp = 0; smp < spp; smp++) {
         uint32_t seed = pixel_seed(W, H, px, smp, spp, frame);
         ray_t r = primary_ray(c, x, y, &seed);
-        res = add(res, s->integrator ? whitted(s, &r, depth, &seed, k) : trace(s, &r, 1, depth, &seed, k));
+        res = add(res, s->integrator == 1 ? whitted(s, &r, depth, &seed, k) : trace(s, &r, 1, depth, &seed, k));
     }
     return smul(1.0f / (float)spp, res);
 }
@@ -994,6 +1104,19 @@ static inline uint32_t rgb8(const float *a) {
     return (r << 16) + (g << 8) + b;
 }
 
+/* running average + RGB8, renderer.cpp:235-241 */
+static void accumulate(float *acc, uint32_t *out, int px, f3 r) {
+    float *a = acc + 4 * (size_t)px;
+    a[3] += 1;
+    float w = a[3], inv = 1.0f / w;
+    float nx = a[0] + inv * (r.x - a[0]);
+    float ny = a[1] + inv * (r.y - a[1]);
+    float nz = a[2] + inv * (r.z - a[2]);
+    float nw = a[3] + inv * (w - a[3]);
+    a[0] = nx; a[1] = ny; a[2] = nz; a[3] = nw;
+    if (out) out[px] = rgb8(a);
+}
+
 void or_tick(const or_scene *s, const or_camera *c, int W, int H, int spp, int depth, int frame,
              int y0, int y1, float *acc, uint32_t *out, or_stats *st, int threads) {
 #ifdef _OPENMP
@@ -1001,6 +1124,25 @@ void or_tick(const or_scene *s, const or_camera *c, int W, int H, int spp, int d
 #else
     (void)threads;
 #endif
+    if (s->integrator == 2) {   /* packet mode: whole 8x8 tiles; rows [y0, y1) rounded out to tiles */
+        int tx_n = (W + 7) / 8, ty0 = y0 / 8, ty1 = (y1 + 7) / 8;
+        #pragma omp parallel
+        {
+            counters k; memset(&k, 0, sizeof(k));
+            #pragma omp for schedule(dynamic)
+            for (int t = ty0 * tx_n; t < ty1 * tx_n; t++) {
+                f3 tile[64];
+                int tx = t % tx_n, ty = t / tx_n;
+                packet_tile(s, c, W, H, spp, depth, frame, tx, ty, tile, &k);
+                for (int l = 0; l < 64; l++) {
+                    int x = tx * 8 + (l & 7), y = ty * 8 + (l >> 3);
+                    if (x < W && y < H) accumulate(acc, out, x + y * W, tile[l]);
+                }
+            }
+            add_counters(st, &k);
+        }
+        return;
+    }
     #pragma omp parallel
     {
         counters k; memset(&k, 0, sizeof(k));
@@ -1008,16 +1150,7 @@ void or_tick(const or_scene *s, const or_camera *c, int W, int H, int spp, int d
         for (int y = y0; y < y1; y++) {
             for (int x = 0; x < W; x++) {
                 int px = x + y * W;
-                f3 r = trace_pixel(s, c, W, H, spp, depth, frame, px, &k);
-                float *a = acc + 4 * (size_t)px;   /* renderer.cpp:237-240 */
-                a[3] += 1;
-                float w = a[3], inv = 1.0f / w;
-                float nx = a[0] + inv * (r.x - a[0]);
-                float ny = a[1] + inv * (r.y - a[1]);
-                float nz = a[2] + inv * (r.z - a[2]);
-                float nw = a[3] + inv * (w - a[3]);
-                a[0] = nx; a[1] = ny; a[2] = nz; a[3] = nw;
-                if (out) out[px] = rgb8(a);
+                accumulate(acc, out, px, trace_pixel(s, c, W, H, spp, depth, frame, px, &k));
             }
         }
         add_counters(st, &k);
@@ -1034,6 +1167,27 @@ void or_intersect(const or_scene *s, const float *R, int n, float *t, int32_t *o
         t[i] = r.t; obj[i] = r.obj; u[i] = r.u; v[i] = r.v;
     }
 }
+void or_intersect_packets(const or_scene *s, const float *R, int n, float *t, int32_t *obj, float *u, float *v) {
+    int np = (n + 63) / 64;
+    #pragma omp parallel for schedule(dynamic, 16)
+    for (int pk = 0; pk < np; pk++) {
+        ray_t P[64];
+        int active[64];
+        for (int l = 0; l < 64; l++) {
+            int i = pk * 64 + l;
+            active[l] = i < n;
+            if (!active[l]) continue;
+            const float *q = R + 7 * (size_t)i;
+            P[l] = mkray(mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), q[6]);
+        }
+        intersect_packet(s, P, active, NULL);
+        for (int l = 0; l < 64; l++) {
+            int i = pk * 64 + l;
+            if (i < n) { t[i] = P[l].t; obj[i] = P[l].obj; u[i] = P[l].u; v[i] = P[l].v; }
+        }
+    }
+}
+
 void or_occluded(const or_scene *s, const float *R, int n, uint8_t *out) {
     #pragma omp parallel for schedule(dynamic, 64)
     for (int i = 0; i < n; i++) {

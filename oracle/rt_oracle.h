@@ -86,7 +86,8 @@ or_scene *or_scene_recipe(const char *name, const char *mesh_dir);
 int or_mesh_read(const char *path, float **verts, int *nv, int **tris, int *nt);
 int or_mesh_write(const char *path, const float *verts, int nv, const int *tris, int nt);
 
-/* integrator used by or_trace_pixels / or_tick: 0 = Trace (default), 1 = WhittedTrace */
+/* integrator used by or_trace_pixels / or_tick: 0 = Trace (default), 1 = WhittedTrace,
+ * 2 = packet mode (IntersectBVHPacket + TracePacket; depth = the bounces' Trace depth) */
 void or_scene_set_integrator(or_scene *s, int mode);
 
 /* camera (camera.h:28-52) */
@@ -107,6 +108,8 @@ void or_tick(const or_scene *s, const or_camera *c, int W, int H, int spp, int d
              int y0, int y1, float *acc, uint32_t *rgb8, or_stats *st, int threads);
 /* batched IntersectBVH / IsOccluded on explicit rays: ray = O.xyz D.xyz tmax */
 void or_intersect(const or_scene *s, const float *rays7, int n, float *t, int32_t *obj, float *u, float *v, int brute);
+/* Scene::IntersectBVHPacket on packets of 64 consecutive rays (the last may be partial) */
+void or_intersect_packets(const or_scene *s, const float *rays7, int n, float *t, int32_t *obj, float *u, float *v);
 void or_occluded(const or_scene *s, const float *rays7, int n, uint8_t *out);
 /* reference probe with the shipped single global RNG (template/template.cpp:674-695),
  * sequence as SURVEY.md Appendix A's driver: coverage pass, then one mode pass. */

@@ -36,15 +36,18 @@ def main():
     np.savez_compressed(os.path.join(HERE, "teapotF_1080p_hits.npz"), pixels=px, rays=rays, t=t, obj=obj, u=u, v=v,
                         occl_rays=occl_rays, occluded=occ)
     # 2. frame checksums: RGB8 CRC32, accumulator sum, ray counts
-    #    (whitted: Renderer::WhittedTrace, the K-key integrator, renderer.cpp:138-195)
-    for recipe, W, H, spp, depth, whitted in (("teapotF", 1920, 1080, 1, 1, 0), ("teapotF", 320, 180, 1, 10, 0),
-                                              ("cfg3", 256, 144, 4, 4, 0), ("mig16", 480, 270, 1, 1, 0),
-                                              ("cfg3", 256, 144, 1, 20, 1), ("teapotF", 320, 180, 1, 20, 1)):
+    #    (whitted: Renderer::WhittedTrace, the K-key integrator, renderer.cpp:138-195;
+    #     packet: the PACKET_TRAVERSAL Tick, renderer.cpp:247-285, with partial edge packets at 250x140)
+    suffix = {0: "", 1: "_whitted", 2: "_packet"}
+    for recipe, W, H, spp, depth, mode in (("teapotF", 1920, 1080, 1, 1, 0), ("teapotF", 320, 180, 1, 10, 0),
+                                           ("cfg3", 256, 144, 4, 4, 0), ("mig16", 480, 270, 1, 1, 0),
+                                           ("cfg3", 256, 144, 1, 20, 1), ("teapotF", 320, 180, 1, 20, 1),
+                                           ("teapotF", 320, 180, 1, 10, 2), ("cfg3", 250, 140, 2, 4, 2)):
         sc = pyoracle.Scene(recipe, DATA_DIR)
-        sc.set_integrator(whitted)
+        sc.set_integrator(mode)
         acc = np.zeros((W * H, 4), np.float32)
         rgb, st = sc.tick(W, H, acc, spp=spp, depth=depth, frame=0)
-        key = f"{recipe}_{W}x{H}_spp{spp}_d{depth}" + ("_whitted" if whitted else "")
+        key = f"{recipe}_{W}x{H}_spp{spp}_d{depth}" + suffix[mode]
         out[key] = {"rgb8_crc32": zlib.crc32(rgb.astype("<u4").tobytes()), "acc_sum": float(acc[:, :3].astype(np.float64).sum()),
                     "shadow": st["shadow"], "bounce": st["isect"] - W * H * spp}
     with open(os.path.join(HERE, "frames.json"), "w") as f:

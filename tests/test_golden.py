@@ -22,13 +22,16 @@ def frames():
         return json.load(f)
 
 
+MODES = {"path": 0, "whitted": 1, "packet": 2}
+
+
 def parse_key(key):
-    """'{recipe}_{W}x{H}_spp{n}_d{depth}[_whitted]' -> (recipe, W, H, spp, depth, whitted)"""
+    """'{recipe}_{W}x{H}_spp{n}_d{depth}[_whitted|_packet]' -> (recipe, W, H, spp, depth, mode)"""
     parts = key.split("_")
-    whitted = parts[-1] == "whitted"
+    mode = MODES[parts[4]] if len(parts) > 4 else 0
     recipe, size, spp, depth = parts[:4]
     W, H = map(int, size.split("x"))
-    return recipe, W, H, int(spp[3:]), int(depth[1:]), whitted
+    return recipe, W, H, int(spp[3:]), int(depth[1:]), mode
 
 
 def test_oracle_reproduces_golden_hits(oracle, rt):
@@ -42,12 +45,13 @@ def test_oracle_reproduces_golden_hits(oracle, rt):
 
 
 @pytest.mark.parametrize("key", ["teapotF_320x180_spp1_d10", "cfg3_256x144_spp4_d4", "mig16_480x270_spp1_d1",
-                                 "cfg3_256x144_spp1_d20_whitted", "teapotF_320x180_spp1_d20_whitted"])
+                                 "cfg3_256x144_spp1_d20_whitted", "teapotF_320x180_spp1_d20_whitted",
+                                 "teapotF_320x180_spp1_d10_packet", "cfg3_250x140_spp2_d4_packet"])
 def test_oracle_reproduces_golden_frames(oracle, rt, key):
-    recipe, W, H, spp, depth, whitted = parse_key(key)
+    recipe, W, H, spp, depth, mode = parse_key(key)
     want = frames()[key]
     s = oracle.Scene(recipe, rt.DATA_DIR)
-    s.set_integrator(int(whitted))
+    s.set_integrator(mode)
     acc = np.zeros((W * H, 4), np.float32)
     rgb, st = s.tick(W, H, acc, spp=spp, depth=depth, frame=0)
     assert zlib.crc32(rgb.astype("<u4").tobytes()) == want["rgb8_crc32"]
@@ -75,11 +79,11 @@ def test_gpu_matches_golden_frames(rt, key):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    recipe, W, H, spp, depth, whitted = parse_key(key)
+    recipe, W, H, spp, depth, mode = parse_key(key)
     want = frames()[key]
     sc = rt.Scene.recipe(recipe)
     r = rt.Renderer(sc, W, H)
-    r.useWhitted = whitted
+    r.mode = mode
     rgb = r.tick_host(spp=spp, depth=depth, frame=0)
     c = r.counters()
     assert c["shadow"] == want["shadow"] and c["bounce"] == want["bounce"]

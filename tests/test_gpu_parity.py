@@ -97,10 +97,11 @@ def test_empty_batches(scenes, torch):
     assert g.IsOccluded(np.zeros((0, 7), np.float32)).numel() == 0
 
 
-def frame_vs_oracle(rt, g, o, W, H, spp, depth, frames=1, exact=True, whitted=False):
+def frame_vs_oracle(rt, g, o, W, H, spp, depth, frames=1, exact=True, whitted=False, mode=None):
+    mode = (rt.MODE_WHITTED if whitted else rt.MODE_PATH) if mode is None else mode
     r = rt.Renderer(g, W, H)
-    r.useWhitted = whitted
-    o.set_integrator(int(whitted))
+    r.mode = mode
+    o.set_integrator(mode)
     acc = np.zeros((W * H, 4), np.float32)
     total = {}
     for f in range(frames):
@@ -301,3 +302,71 @@ def test_invalid_scenes_rejected(rt, torch):
         rt.Scene([rt.sphere((0, 0, 0), 1, 5)], mats)   # material out of range
     with pytest.raises(rt.RTError):
         rt.Scene([rt.sphere((0, 0, 0), 1, 0)], mats, sky=np.zeros((3, 5), np.uint32))   # not power of two
+
+
+# ---- Scene::IntersectBVHPacket (template/scene.h:322-412) and the PACKET_TRAVERSAL Tick
+def tile_order_pixels(W, H):
+    """pixel ids in 8x8-tile order: consecutive runs of 64 = the reference's packets"""
+    tx, ty, lane = np.arange((W + 7) // 8), np.arange((H + 7) // 8), np.arange(64)
+    x = tx[None, :, None] * 8 + lane[None, None, :] % 8
+    y = ty[:, None, None] * 8 + lane[None, None, :] // 8
+    x, y = np.broadcast_arrays(x, y)
+    keep = (x < W) & (y < H)
+    return (y * W + x)[keep].astype(np.int32)
+
+
+@pytest.mark.parametrize("name", ["teapotF", "cfg3", "mig16"])
+def test_packet_camera_rays_bit_exact(scenes, name):
+    g, o = scenes(name)
+    W, H = 1920, 1080
+    rays = o.camera_rays(W, H, tile_order_pixels(W, H))
+    want = o.intersect_packets(rays)
+    hits_equal(g.IntersectBVHPacket(rays), want)
+    # the packet result is the closest hit: same as the single-ray traversal here
+    assert np.array_equal(want[1], o.intersect(rays)[1])
+
+
+def test_packet_random_rays_and_partial_packet(scenes):
+    g, o = scenes("cfg3")
+    for n in (64 * 700 + 37, 5, 64):
+        rays = random_rays(n, n)
+        hits_equal(g.IntersectBVHPacket(rays), o.intersect_packets(rays))
+    hits = g.intersect_packets_host(random_rays(130, 3))
+    want = o.intersect_packets(random_rays(130, 3))
+    assert np.array_equal(hits["obj"], want[1])
+
+
+def packet_check(rt, g, o, W, H, spp, depth, frames=1):
+    got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, W, H, spp, depth, frames=frames, mode=rt.MODE_PACKET)
+    d = np.abs(gacc - acc)
+    assert d.max() <= PIX_TOL, d.max()
+    assert np.array_equal(got, want), f"{(got != want).sum()} RGB8 mismatches"
+    assert c["shadow"] == st["shadow"]
+    assert c["bounce"] == st["isect"] - W * H * spp * frames
+
+
+def test_packet_mode_teapot_depth10(rt, scenes):
+    g, o = scenes("teapotF")
+    packet_check(rt, g, o, 320, 180, 1, 10)
+
+
+def test_packet_mode_depth0_and_edges(rt, scenes):
+    g, o = scenes("cfg3")
+    packet_check(rt, g, o, 250, 140, 2, 0)     # primary + NEE only; partial edge packets
+    packet_check(rt, g, o, 250, 140, 1, 4, frames=2)
+
+
+def test_packet_mode_mix_material_textured_sky(rt, oracle, torch):
+    """Checkerboard with diffuse 0.5 is MIX: a specular bounce is traced twice (renderer.cpp:111-120)."""
+    g, o = sky_scene(rt, oracle)
+    packet_check(rt, g, o, 96, 60, 2, 5)
+    g, o = glass_scene(rt, oracle)
+    packet_check(rt, g, o, 100, 70, 1, 12)
+
+
+def test_compat_host_program_on_gpu(rt, torch, tmp_path):
+    from test_host import build_compat_host
+    import subprocess
+    exe = build_compat_host(rt, tmp_path)
+    r = subprocess.run([exe, rt.DATA_DIR], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -36,13 +36,23 @@ def test_library_is_gfx950_code_object(rt):
     assert "gfx950" in text
 
 
-def test_compat_header_compiles(rt, tmp_path):
-    src = tmp_path / "t.cpp"
-    src.write_text('#include "rt_compat.hpp"\nint main(){ Tmpl8::Camera c(64, 32); return c.cam.lens_radius > 0 ? 0 : 1; }\n')
-    exe = tmp_path / "t"
-    subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
+def build_compat_host(rt, tmp_path):
+    exe = tmp_path / "compat_host"
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "compat_host.cpp"), "-o", str(exe),
                     rt.LIB_PATH, f"-Wl,-rpath,{os.path.dirname(rt.LIB_PATH)}"], check=True)
-    assert subprocess.run([str(exe)]).returncode == 0
+    return str(exe)
+
+
+def test_compat_header_compiles(rt, tmp_path):
+    """The reference-shaped C++ host builds against the header and links the library;
+    without a GPU it must fail loudly with RT_ERR_NO_DEVICE (exit 3), never fall back."""
+    exe = build_compat_host(rt, tmp_path)
+    r = subprocess.run([exe, rt.DATA_DIR], capture_output=True, text=True)
+    if rt.device_count() == 0:
+        assert r.returncode == 3, r.stdout
+    else:
+        assert r.returncode == 0, r.stdout
 
 
 def test_abi_version_and_device_count(rt):

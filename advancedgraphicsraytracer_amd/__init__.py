@@ -27,6 +27,7 @@ DIFFUSE, MIRROR, DIELECTRIC, CHECKERBOARD, LIGHT = 0, 1, 2, 3, 4
 MODE_PATH = 0
 MODE_WHITTED = 1
 MODE_PACKET = 2
+WALK_LANE, WALK_WAVE = 0, 1
 # renderer.h:9, renderer.h:13, renderer.cpp:105 (TracePacket's bounces: Trace's default depth)
 DEFAULT_DEPTH = {MODE_PATH: 10, MODE_WHITTED: 20, MODE_PACKET: 10}
 RECIPES = ("teapotF", "teapot", "mig16", "cfg3", "cfg5")
@@ -115,6 +116,7 @@ def lib():
         "rt_scene_create_recipe": ([C.c_char_p, C.c_char_p, i32, C.POINTER(vp)], C.c_int),
         "rt_scene_destroy": ([vp], C.c_int),
         "rt_scene_get_info": ([vp, C.POINTER(SceneInfo)], C.c_int),
+        "rt_scene_set_camera_walk": ([vp, C.c_int], C.c_int),
         "rt_scene_copy_bvh": ([vp, vp, C.POINTER(u32)], C.c_int),
         "rt_intersect": ([vp, vp, vp, u32, vp], C.c_int),
         "rt_occluded": ([vp, vp, vp, u32, vp], C.c_int),
@@ -369,6 +371,10 @@ class Scene:
             s = stream if stream is not None else torch.cuda.current_stream(r.device).cuda_stream
             _check(self.L.rt_intersect(self.h, C.c_void_p(r.data_ptr()), C.c_void_p(hits.data_ptr()), n, C.c_void_p(s)))
         return hits[:, 0], hits.view(torch.int32)[:, 1], hits[:, 2], hits[:, 3]
+
+    def set_camera_walk(self, walk):
+        """WALK_LANE (default) or WALK_WAVE: how camera rays walk the BVH (same results)."""
+        _check(self.L.rt_scene_set_camera_walk(self.h, walk))
 
     def IntersectBVHPacket(self, rays, stream=None):
         """Batched Scene::IntersectBVHPacket: rays [64k, 64k+64) form packet k."""

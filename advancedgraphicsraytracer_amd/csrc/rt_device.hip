@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -59,6 +60,7 @@ struct SceneView {
     int bounds_finite;                  // every node bound is a finite float
     uint32_t stack_entries;             // LDS stack entries per lane
     uint32_t node_f4;                   // node array size in float4s
+    int wave_primary;                   // camera rays take the wave-coherent walk
 };
 
 struct FrameArgs {
@@ -170,6 +172,50 @@ __device__ __forceinline__ void prim_intersect(const SceneView &S, uint32_t k, D
     } else {
         f3 N = mk(p0.x, p0.y, p0.z);
         float t = -(dot(r.O, N) + p1.x) / (dot(r.D, N));
+        if (t < r.t && t > kEPS) { r.t = t; r.obj = id; }
+    }
+}
+
+// prim_intersect plus `tie`: set when the candidate distance equals the current r.t
+// exactly (a second primitive at the same distance: the visiting order would decide).
+__device__ __forceinline__ void prim_intersect_t(const SceneView &S, uint32_t k, DRay &r, bool &tie) {
+    float4 p0 = S.prims[3 * k], p1 = S.prims[3 * k + 1];
+    uint32_t type = __float_as_uint(p1.w);
+    int id = __float_as_int(p0.w);
+    if (type == T_TRI) {
+        float4 p2 = S.prims[3 * k + 2];
+        f3 A = mk(p0.x, p0.y, p0.z), AB = mk(p1.x, p1.y, p1.z), AC = mk(p2.x, p2.y, p2.z);
+        float denom = dot(cross(r.D, AC), AB);
+        if (fabsf(denom) < kDENOM_EPS) return;
+        f3 AO = r.O - A;
+        float u = dot(cross(-r.D, AO), AC) / denom;
+        if (u < 0 || u > 1) return;
+        float v = dot(cross(-r.D, AB), AO) / denom;
+        if (v < 0 || u + v > 1) return;
+        float t = dot(cross(AO, AB), AC) / denom;
+        if (t <= r.t && t > kEPS) {
+            if (t == r.t) tie = true;
+            else { r.t = t; r.obj = id; r.u = u; r.v = v; }
+        }
+    } else if (type == T_SPH) {
+        f3 oc = r.O - mk(p0.x, p0.y, p0.z);
+        float b = dot(oc, r.D);
+        float c = dot(oc, oc) - p1.x;
+        float d = b * b - c;
+        if (d <= 0) return;
+        d = sqrtf(d);
+        float t = -b - d;
+        if (t == r.t && t > kEPS) tie = true;
+        if (!(t < r.t && t > kEPS)) {
+            t = d - b;
+            if (t == r.t && t > kEPS) tie = true;
+            if (!(t < r.t && t > kEPS)) return;
+        }
+        r.t = t; r.obj = id;
+    } else {
+        f3 N = mk(p0.x, p0.y, p0.z);
+        float t = -(dot(r.O, N) + p1.x) / (dot(r.D, N));
+        if (t == r.t && t > kEPS) tie = true;
         if (t < r.t && t > kEPS) { r.t = t; r.obj = id; }
     }
 }
@@ -287,10 +333,84 @@ __device__ __forceinline__ bool occluded_t(const SceneView &S, const Trav<STRIDE
     }
 }
 
+// ---- wave-coherent closest hit: the calling lanes walk the union of their subtrees with
+// a wave-uniform node and stack (the stack lives in the LDS column of the wave's lane 0 --
+// a VGPR lane-stack cannot be used because the caller may have lanes switched off).
+// Closest hit along the union of the lanes' subtrees; children are visited in the order
+// most calling lanes prefer.  A lane tests a leaf only if its slab test passed with its t
+// at that moment.  Results equal IntersectBVH's whenever the closest hit is unique: `tie`
+// reports a lane that met a second primitive at exactly its current t, and `odd` a hit
+// nearer than its leaf box's entry distance (float rounding at a box face) -- the two
+// ways the visiting order could matter; such lanes are re-traced in the reference order.
+template <int STRIDE>
+__device__ __forceinline__ void wave_closest_hit_fast(const SceneView &S, const Trav<STRIDE> &T, DRay &r, bool &flag) {
+    const float4 *nodes = T.nodes;
+    uint32_t *ws = T.stk - __lane_id();               // the wave's uniform stack (node indices)
+    uint32_t word = __builtin_amdgcn_readfirstlane(S.root_word);
+    bool in = true;
+    float tb = -1e30f;                                // my slab entry distance of the current node
+    uint32_t sp = 0;
+    for (;;) {
+        const uint32_t cnt = word & 0xffu, lf = word >> 8;
+        if (cnt) {
+            if (in)
+                for (uint32_t k = lf; k < lf + cnt; ++k) {
+                    const float t0 = r.t;
+                    prim_intersect_t(S, k, r, flag);
+                    if (r.t != t0 && r.t < tb) flag = true;   // hit nearer than its box's entry
+                }
+        } else {
+            const float4 *q = nodes + 2 * lf;
+            const float4 a0 = q[0], b0 = q[1], a1 = q[2], b1 = q[3];
+            const float d1 = in ? slab_dist<true>(r, a0, b0) : 1e30f, d2 = in ? slab_dist<true>(r, a1, b1) : 1e30f;
+            const bool h1 = d1 != 1e30f, h2 = d2 != 1e30f;
+            const uint64_t m1 = __ballot(h1), m2 = __ballot(h2);
+            if (m1 | m2) {
+                const uint32_t v1 = __popcll(__ballot(h1 && !(h2 && d2 < d1)));
+                const uint32_t v2 = __popcll(__ballot(h2 && !(h1 && d1 <= d2)));
+                const bool first1 = m1 && (!m2 || v1 >= v2);
+                if (m1 && m2) {
+                    ws[sp * STRIDE] = first1 ? lf + 1 : lf;
+                    ++sp;
+                }
+                word = __builtin_amdgcn_readfirstlane(__float_as_uint(first1 ? b0.z : b1.z));
+                in = first1 ? h1 : h2;
+                tb = first1 ? d1 : d2;
+                continue;
+            }
+        }
+        // pop, re-testing each entry with the lanes' current t
+        for (;;) {
+            if (sp == 0) return;
+            --sp;
+            const uint32_t ni = __builtin_amdgcn_readfirstlane(ws[sp * STRIDE]);
+            const float4 a = nodes[2 * ni], b = nodes[2 * ni + 1];
+            tb = slab_dist<true>(r, a, b);
+            in = tb != 1e30f;
+            if (__ballot(in)) {
+                word = __builtin_amdgcn_readfirstlane(__float_as_uint(b.z));
+                break;
+            }
+        }
+    }
+}
+
 template <int STRIDE>
 __device__ __forceinline__ void closest_hit(const SceneView &S, const Trav<STRIDE> &T, DRay &r) {
     if (__all(S.bounds_finite && ray_finite(r))) closest_hit_t<true>(S, T, r);
     else closest_hit_t<false>(S, T, r);
+}
+// camera rays: the wave-coherent walk where the scene asks for it (SceneView::wave_primary)
+template <int STRIDE>
+__device__ __forceinline__ void closest_hit_primary(const SceneView &S, const Trav<STRIDE> &T, DRay &r) {
+    if (S.wave_primary && __all(S.bounds_finite && ray_finite(r))) {
+        const DRay r0 = r;
+        bool flag = false;
+        wave_closest_hit_fast(S, T, r, flag);
+        if (flag) { r = r0; closest_hit_t<true>(S, T, r); }
+        return;
+    }
+    closest_hit(S, T, r);
 }
 template <int STRIDE>
 __device__ __forceinline__ bool occluded(const SceneView &S, const Trav<STRIDE> &T, const DRay &r) {
@@ -303,7 +423,8 @@ __device__ __forceinline__ bool occluded(const SceneView &S, const Trav<STRIDE> 
 // packet.  The node, the stack and the "first active" ray are wave-uniform (node and
 // primitive loads are scalar, the stack lives in one VGPR: entry i in lane i); each lane
 // tests its own ray and a ballot finds the lowest hitting lane.  Inactive lanes (past the
-// end of the batch / off screen) never test and never lead.
+// end of the batch / off screen) never test and never lead.  The VGPR lane-stack needs all
+// 64 lanes switched on: callers invoke it from wave-uniform control flow only.
 __device__ __forceinline__ float readlane_f(float v, uint32_t l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
 }
@@ -497,7 +618,7 @@ __device__ __forceinline__ f3 nee(const SceneView &S, const Trav<STRIDE> &T, f3 
 // Renderer::Trace (renderer.cpp:17-72) as a loop.  The recursion's result
 // BRDF * ((Trace * dot) / PDF) + Ld is folded innermost-first from per-level records,
 // so the float evaluation order is the reference's.
-template <int MAXD, bool TEX_SKY, int STRIDE>
+template <int MAXD, bool TEX_SKY, int STRIDE, bool CAMWAVE = false>
 __device__ f3 trace_path(const SceneView &S, const Trav<STRIDE> &T, DRay ray, int depth, uint32_t &seed,
                          uint32_t &nshadow, uint32_t &nbounce, bool lastSpec = true) {
     f3 lv_mul[MAXD], lv_add[MAXD];
@@ -507,7 +628,8 @@ __device__ f3 trace_path(const SceneView &S, const Trav<STRIDE> &T, DRay ray, in
     f3 term = mk(0, 0, 0);
     for (int d = depth; d > 0 && levels < MAXD; --d) {
         if (d != depth) ++nbounce;
-        closest_hit(S, T, ray);
+        if (CAMWAVE && d == depth) closest_hit_primary(S, T, ray);
+        else closest_hit(S, T, ray);
         if (ray.obj == -1) { term = sky_color<TEX_SKY>(S, ray.D); break; }
         f3 I = ray.O + ray.t * ray.D;
         float4 s0 = S.shade[2 * ray.obj], s1 = S.shade[2 * ray.obj + 1];
@@ -783,6 +905,9 @@ __device__ __forceinline__ void render_tile(const SceneView &S, const FrameArgs 
     const uint32_t x = (tile % F.tiles_x) * 8u + (lane & 7u), y = (tile / F.tiles_x) * 8u + (lane >> 3);
     const bool on = x < F.W && y < F.H;
     const uint32_t px = x + y * F.W;
+    // the wave-coherent camera-ray walk is compiled into the global-node primary+shadow
+    // kernel only (SceneView::wave_primary picks it at run time)
+    constexpr bool kCamWave = MODE == M_PATH && MAXD == 1 && STRIDE == 256;
     uint32_t nshadow = 0, nbounce = 0;
     f3 sum = mk(0, 0, 0);
     if (MODE == M_PACKET) {                           // the traversal is wave-wide: no early exit
@@ -797,7 +922,7 @@ __device__ __forceinline__ void render_tile(const SceneView &S, const FrameArgs 
             uint32_t seed = init_seed(px + F.W * F.H * (s + F.spp * F.frame));
             DRay ray = primary_ray(F, x, y, seed);
             if constexpr (MODE == M_WHITTED) sum = sum + trace_whitted<TEX_SKY>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
-            else sum = sum + trace_path<MAXD, TEX_SKY>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
+            else sum = sum + trace_path<MAXD, TEX_SKY, STRIDE, kCamWave>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
         }
     }
     if (on) {
@@ -1210,6 +1335,9 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 #ifndef RT_DISABLE_LDS_SCENE
     s->lds_nodes = (size_t)s->stack_depth * 4096u + (size_t)s->bvh.nodes_used * 32u <= 160u * 1024u;
 #endif
+    // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
+    v.wave_primary = 0;
+    if (const char *e = std::getenv("RT_WAVE_PRIMARY")) v.wave_primary = std::atoi(e) != 0;
     v.bounds_finite = 1;
     for (uint32_t i = 0; i < s->bvh.nodes_used && v.bounds_finite; ++i) {
         if (i == 1) continue;
@@ -1367,6 +1495,13 @@ int rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
     info->nodes_used = s->bvh.nodes_used;
     info->depth = s->bvh.depth;
     info->max_leaf = s->bvh.max_leaf;
+    return RT_OK;
+}
+
+int rt_scene_set_camera_walk(rt_scene *s, int walk) {
+    if (!s) return fail(RT_ERR_INVALID, "null argument");
+    if (walk != RT_WALK_LANE && walk != RT_WALK_WAVE) return fail(RT_ERR_INVALID, "unknown camera walk");
+    s->view.wave_primary = walk == RT_WALK_WAVE;
     return RT_OK;
 }
 

@@ -370,3 +370,15 @@ def test_compat_host_program_on_gpu(rt, torch, tmp_path):
     exe = build_compat_host(rt, tmp_path)
     r = subprocess.run([exe, rt.DATA_DIR], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+# ---- wave-coherent camera-ray walk (rt_scene_set_camera_walk): same frames, same counts
+@pytest.mark.parametrize("name,W,H", [("mig16", 480, 270), ("cfg3", 320, 180), ("cfg5", 333, 201)])
+def test_wave_camera_walk_bit_exact(rt, oracle, torch, name, W, H):
+    g = rt.Scene.recipe(name)
+    g.set_camera_walk(rt.WALK_WAVE)
+    o = oracle.Scene(name, rt.DATA_DIR)
+    got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, W, H, 1, 1, frames=2)
+    assert np.array_equal(got, want)
+    assert np.array_equal(gacc.view(np.uint32), acc.view(np.uint32))
+    assert c["shadow"] == st["shadow"]

@@ -3,9 +3,11 @@
 5.4 rule 24).  Each build is loaded RTLD_LOCAL through raw ctypes; rounds alternate
 between builds; the per-build median and min of the per-frame kernel time are printed.
 
-usage: ab.py LIB [LIB ...] [--scene teapotF] [--w 1920] [--h 1080] [--spp 1] [--depth 1]
-             [--rounds 7] [--frames 20] [--check]
---check compares every build's RGB8 frame with the first build's (bit-exact).
+usage: ab.py LIB[@mode=M,depth=D] [...] [--scene teapotF] [--w 1920] [--h 1080] [--spp 1]
+             [--depth 1] [--rounds 7] [--frames 20] [--check]
+A LIB may carry its own integrator mode (0 path, 1 Whitted, 2 packet) and depth, so one
+build can be timed against itself in another mode.
+--check compares every entry's RGB8 frame with the first entry's (bit-exact).
 """
 import argparse
 import ctypes as C
@@ -46,8 +48,19 @@ def main():
     ap.add_argument("--check", action="store_true")
     a = ap.parse_args()
     builds = []
+    cfg = {}
+    loaded = {}
     for p in a.libs:
-        L = load(p)
+        path, _, opts = p.partition("@")
+        kv = dict(o.split("=") for o in opts.split(",") if o)
+        cfg[p] = (int(kv.get("mode", 0)), int(kv.get("depth", a.depth)))
+        L = loaded.get(path) or load(path)
+        loaded[path] = L
+        for k, v in kv.items():              # upper-case options are environment knobs read at scene creation
+            if k.isupper():
+                os.environ[k] = v
+            elif k not in ("mode", "depth"):
+                raise SystemExit(f"unknown option {k}")
         sc, r = C.c_void_p(), C.c_void_p()
         assert L.rt_scene_create_recipe(a.scene.encode(), rt.DATA_DIR.encode(), 0, C.byref(sc)) == 0, L.rt_last_error()
         assert L.rt_renderer_create(sc, a.w, a.h, C.byref(r)) == 0, L.rt_last_error()
@@ -55,17 +68,21 @@ def main():
         L.rt_camera_default(a.w, a.h, C.byref(cam))
         out = torch.zeros(a.w * a.h, dtype=torch.int32, device="cuda")
         builds.append((p, L, sc, r, cam, out))
+        for k in kv:
+            if k.isupper():
+                del os.environ[k]
     times = {p: [] for p in a.libs}
     frame = 0
     for rnd in range(a.rounds):
         for p, L, sc, r, cam, out in builds:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             # warm + timed frames on the default stream
-            fp = rt.FrameParams(a.w, a.h, a.spp, a.depth, frame, 0, 0)
+            mode, depth = cfg[p]
+            fp = rt.FrameParams(a.w, a.h, a.spp, depth, frame, mode, 0)
             L.rt_render_frame(r, C.byref(cam), C.byref(fp), C.c_void_p(out.data_ptr()), None)
             ev[0].record()
             for k in range(a.frames):
-                fp = rt.FrameParams(a.w, a.h, a.spp, a.depth, frame + 1 + k, 0, 0)
+                fp = rt.FrameParams(a.w, a.h, a.spp, depth, frame + 1 + k, mode, 0)
                 rc = L.rt_render_frame(r, C.byref(cam), C.byref(fp), C.c_void_p(out.data_ptr()), None)
                 assert rc == 0, L.rt_last_error()
             ev[1].record()
@@ -78,12 +95,12 @@ def main():
         L.rt_renderer_counters(r, C.byref(c))
         t = np.array(times[p])
         rays_per_frame = (c.primary + c.shadow + c.bounce) / max(1, c.frames)
-        res[os.path.basename(p)] = {"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(t.min()), 4),
+        res[os.path.basename(p)] = {"mode": cfg[p][0], "depth": cfg[p][1],"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(t.min()), 4),
                                     "mrays_s": round(rays_per_frame / (np.median(t) * 1e-3) / 1e6, 1)}
     if a.check:
         ref = None
         for p, L, sc, r, cam, out in builds:
-            fr = rt.FrameParams(a.w, a.h, a.spp, a.depth, 12345, 0, 1)
+            fr = rt.FrameParams(a.w, a.h, a.spp, cfg[p][1], 12345, cfg[p][0], 1)
             L.rt_render_frame(r, C.byref(cam), C.byref(fr), C.c_void_p(out.data_ptr()), None)
             torch.cuda.synchronize()
             img = out.cpu().numpy().copy()

@@ -21,9 +21,10 @@ LIB_PATH = os.path.join(PKG_DIR, "librtamd.so")
 DATA_DIR = os.path.join(PKG_DIR, "data")
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "rt_amd.h")
 
+ABI_VERSION = 2   # include/rt_amd.h RT_ABI_VERSION
 RT_OK, RT_ERR_INVALID, RT_ERR_NO_DEVICE, RT_ERR_HIP, RT_ERR_IO, RT_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5
-SPHERE, PLANE, TRIANGLE = 0, 1, 4
-DIFFUSE, MIRROR, DIELECTRIC, CHECKERBOARD, LIGHT = 0, 1, 2, 3, 4
+SPHERE, PLANE, CUBE, QUAD, TRIANGLE = 0, 1, 2, 3, 4
+DIFFUSE, MIRROR, DIELECTRIC, CHECKERBOARD, LIGHT, DSMIX, TEXTURE = 0, 1, 2, 3, 4, 5, 6
 MODE_PATH = 0
 MODE_WHITTED = 1
 MODE_PACKET = 2
@@ -45,7 +46,11 @@ class Prim(C.Structure):
 
 class Material(C.Structure):
     _fields_ = [("kind", C.c_int32), ("color", C.c_float * 3), ("color2", C.c_float * 3), ("ior", C.c_float),
-                ("diffuse", C.c_float)]
+                ("diffuse", C.c_float), ("texture", C.c_int32)]
+
+
+class Texture(C.Structure):
+    _fields_ = [("pixels", C.POINTER(C.c_uint32)), ("width", C.c_uint32), ("height", C.c_uint32)]
 
 
 class SceneDesc(C.Structure):
@@ -53,7 +58,8 @@ class SceneDesc(C.Structure):
                 ("materials", C.POINTER(Material)), ("num_materials", C.c_uint32),
                 ("sky_pixels", C.POINTER(C.c_uint32)), ("sky_width", C.c_uint32), ("sky_height", C.c_uint32),
                 ("bvh_nodes", C.c_void_p), ("bvh_num_nodes", C.c_uint32), ("bvh_indices", C.POINTER(C.c_uint32)),
-                ("device", C.c_int32)]
+                ("device", C.c_int32), ("transforms", C.POINTER(C.c_float)),
+                ("textures", C.POINTER(Texture)), ("num_textures", C.c_uint32)]
 
 
 class SceneInfo(C.Structure):
@@ -111,7 +117,9 @@ def lib():
         "rt_mesh_to_prims": ([fp, u32, C.POINTER(i32), u32, fp, i32, C.POINTER(Prim)], C.c_int),
         "rt_recipe_describe": ([C.c_char_p, C.c_char_p, C.POINTER(Prim), C.POINTER(u32), C.POINTER(Material),
                                 C.POINTER(u32)], C.c_int),
-        "rt_bvh_build_host": ([C.POINTER(Prim), u32, vp, C.POINTER(u32), C.POINTER(SceneInfo)], C.c_int),
+        "rt_bvh_build_host": ([C.POINTER(Prim), C.POINTER(C.c_float), u32, vp, C.POINTER(u32), C.POINTER(SceneInfo)],
+                              C.c_int),
+        "rt_image_load": ([C.c_char_p, C.POINTER(C.POINTER(u32)), C.POINTER(u32), C.POINTER(u32)], C.c_int),
         "rt_scene_create": ([C.POINTER(SceneDesc), C.POINTER(vp)], C.c_int),
         "rt_scene_create_recipe": ([C.c_char_p, C.c_char_p, i32, C.POINTER(vp)], C.c_int),
         "rt_scene_destroy": ([vp], C.c_int),
@@ -141,7 +149,7 @@ def lib():
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
-    if L.rt_abi_version() != 1:
+    if L.rt_abi_version() != ABI_VERSION:
         raise RTError(RT_ERR_INVALID, "librtamd.so ABI mismatch")
     _lib = L
     return L
@@ -243,13 +251,26 @@ def recipe_describe(name, mesh_dir=DATA_DIR):
     return list(pa), list(ma)
 
 
+def _transforms(prims):
+    """per-primitive mat4 array for cubes / quads (None if the scene has none)"""
+    if not any(getattr(p, "T", None) is not None for p in prims):
+        return None
+    T = np.tile(np.eye(4, dtype=np.float32).reshape(16), (len(prims), 1))
+    for i, p in enumerate(prims):
+        if getattr(p, "T", None) is not None:
+            T[i] = np.asarray(p.T, np.float32).reshape(16)
+    return T
+
+
 def build_bvh_host(prims):
     """Plain binned-SAH BVH on the host (template/scene.h:845-976): (nodes[n,32] u8, indices, info)."""
     arr = (Prim * len(prims))(*prims)
+    T = _transforms(prims)
     nodes = np.zeros((2 * len(prims) + 2, 32), np.uint8)
     idx = np.zeros(len(prims), np.uint32)
     info = SceneInfo()
-    _check(lib().rt_bvh_build_host(arr, len(prims), nodes.ctypes.data_as(C.c_void_p),
+    _check(lib().rt_bvh_build_host(arr, None if T is None else T.ctypes.data_as(C.POINTER(C.c_float)), len(prims),
+                                   nodes.ctypes.data_as(C.c_void_p),
                                    idx.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(info)))
     return nodes[:info.nodes_used], idx, _info_dict(info)
 
@@ -277,13 +298,43 @@ def triangle(a, b, c, material):
     return p
 
 
-def material(kind, color=(0, 0, 0), color2=(0, 0, 0), ior=0.0, diffuse=-1.0):
+def material(kind, color=(0, 0, 0), color2=(0, 0, 0), ior=0.0, diffuse=-1.0, texture=-1):
     m = Material(kind)
     m.color[:] = color
     m.color2[:] = color2
     m.ior = ior
     m.diffuse = diffuse
+    m.texture = texture
     return m
+
+
+def cube(pos, size, material, T=None):
+    """Primitive::createCube(pos, size, material, T) (Primitive.h:717-728)"""
+    p = Prim(CUBE, material)
+    p.v[0], p.v[1], p.v[2] = pos
+    p.v[3], p.v[4], p.v[5] = (size, size, size) if np.isscalar(size) else size
+    p.T = None if T is None else np.asarray(T, np.float32).reshape(16)
+    return p
+
+
+def quad(size, material, T=None):
+    """Primitive::createQuad(size, material, T) (Primitive.h:735-739)"""
+    p = Prim(QUAD, material)
+    p.v[0] = size
+    p.T = None if T is None else np.asarray(T, np.float32).reshape(16)
+    return p
+
+
+def load_image(path):
+    """Surface(file) / Surface::LoadImage (template/template.cpp:1571-1601): uint32 [h, w] 0x00RRGGBB."""
+    L = lib()
+    px = C.POINTER(C.c_uint32)()
+    w, h = C.c_uint32(), C.c_uint32()
+    _check(L.rt_image_load(os.fsencode(path), C.byref(px), C.byref(w), C.byref(h)))
+    try:
+        return np.ctypeslib.as_array(px, shape=(h.value, w.value)).copy()
+    finally:
+        L.rt_free(px)
 
 
 # ---------------------------------------------------------------- device objects
@@ -304,7 +355,9 @@ def _as_device_rays(rays, device):
 class Scene:
     """Scene (template/scene.h:37): primitives + materials + plain BVH, resident in HBM."""
 
-    def __init__(self, prims=None, materials=None, sky=None, bvh=None, device=0, _handle=None):
+    def __init__(self, prims=None, materials=None, sky=None, bvh=None, device=0, textures=(), _handle=None):
+        """prims: Prim records (cube()/quad() carry their mat4 in .T); textures: uint32 [h, w]
+        arrays of 0x00RRGGBB referenced by texture_material(index)."""
         self.L = lib()
         self.device = device
         self.h = C.c_void_p()
@@ -323,6 +376,18 @@ class Scene:
             d.sky_pixels = sky.ctypes.data_as(C.POINTER(C.c_uint32))
             d.sky_height, d.sky_width = sky.shape
             keep.append(sky)
+        T = _transforms(prims)
+        if T is not None:
+            d.transforms = T.ctypes.data_as(C.POINTER(C.c_float))
+            keep.append(T)
+        if len(textures):
+            texs = [np.ascontiguousarray(t, np.uint32) for t in textures]
+            ta = (Texture * len(texs))()
+            for k, t in enumerate(texs):
+                ta[k].pixels = t.ctypes.data_as(C.POINTER(C.c_uint32))
+                ta[k].height, ta[k].width = t.shape
+            d.textures, d.num_textures = ta, len(texs)
+            keep += texs + [ta]
         if bvh is not None:
             nodes, idx = np.ascontiguousarray(bvh[0], np.uint8), np.ascontiguousarray(bvh[1], np.uint32)
             d.bvh_nodes = nodes.ctypes.data_as(C.c_void_p)

@@ -18,6 +18,7 @@ HEADERS = ["rt_math.h", "rt_internal.h", "rt_libm.h", os.path.join("..", "..", "
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off + IEEE div/sqrt (hipcc's default) keep the kernels' float results
 # bit-identical to the reference's evaluation order.
+LIBS = ["-lz"]   # zlib: PNG textures (rt_image_load)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
          "-Wall", "-Wno-unused-function"]
 
@@ -33,7 +34,7 @@ def _stale():
 def build(force=False, verbose=False):
     if not force and not _stale():
         return LIB
-    cmd = [HIPCC] + FLAGS + ["-o", LIB + ".tmp"] + [os.path.join(CSRC, f) for f in SOURCES]
+    cmd = [HIPCC] + FLAGS + ["-o", LIB + ".tmp"] + [os.path.join(CSRC, f) for f in SOURCES] + LIBS
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -34,13 +34,14 @@
 
 namespace rt {
 
-enum : uint32_t { T_TRI = 4, T_SPH = 0, T_PLANE = 1 };
+enum : uint32_t { T_TRI = 4, T_SPH = 0, T_PLANE = 1, T_CUBE = 2, T_QUAD = 3 };
 enum : int { F_DIFFUSE = 0, F_SPECULAR = 1, F_MIX = 2, F_DIELECTRIC = 3, F_LIGHT = 4 };
 
 struct DevMaterial {
     int kind, flag;
     float c0[3], c1[3];
-    float ior, diffuse, specular, pad;
+    float ior, diffuse, specular;
+    uint32_t tex_off, tex_w, tex_h;   // TextureMaterial: texels at SceneView::tex + tex_off
 };
 
 struct SceneView {
@@ -49,13 +50,18 @@ struct SceneView {
     const float4 *__restrict__ shade;   // 2 float4 per primitive id
     const DevMaterial *__restrict__ mats;
     const uint32_t *__restrict__ sky;
+    const float4 *__restrict__ xprims;  // cubes / quads: 8 float4 each (Minv rows, M rows, data)
+    const uint32_t *__restrict__ tex;   // all TextureMaterial texels
     uint32_t sky_w, sky_h;
     int sky_const;
     float sky_rgb[3];
-    float light_M[12];                  // prim 0 Transform rows 0..2 (Translate)
+    float light_M[12];                  // prim 0 Transform rows 0..2
     float light_c[3];
     float light_r, light_r2, light_invr;
     int light_mat;
+    int light_quad;                     // prim 0 is a quad (else a sphere)
+    float light_qsize, light_area;      // quad data[0].x; Primitive::GetArea
+    float light_N[3];                   // quad normal TransformVector((0,-1,0), M)
     uint32_t root_word;
     int bounds_finite;                  // every node bound is a finite float
     uint32_t stack_entries;             // LDS stack entries per lane
@@ -140,6 +146,79 @@ __device__ __forceinline__ bool ray_finite(const DRay &r) {
 }
 
 // ------------------------------------------------------------------ primitive tests (Primitive.h:64-279)
+// TransformPosition / TransformVector with the matrix as three float4 rows (same order of
+// operations as rt_math.h tpos / tvec)
+__device__ __forceinline__ f3 tpos_rows(float4 r0, float4 r1, float4 r2, f3 a) {
+    return mk(r0.x * a.x + r0.y * a.y + r0.z * a.z + r0.w * 1.0f, r1.x * a.x + r1.y * a.y + r1.z * a.z + r1.w * 1.0f,
+              r2.x * a.x + r2.y * a.y + r2.z * a.z + r2.w * 1.0f);
+}
+__device__ __forceinline__ f3 tvec_rows(float4 r0, float4 r1, float4 r2, f3 a) {
+    return mk(r0.x * a.x + r0.y * a.y + r0.z * a.z + r0.w * 0.0f, r1.x * a.x + r1.y * a.y + r1.z * a.z + r1.w * 0.0f,
+              r2.x * a.x + r2.y * a.y + r2.z * a.z + r2.w * 0.0f);
+}
+// CUBE slab test in object space (Primitive.h:87-110 / 196-235); false on a miss
+__device__ __forceinline__ bool cube_slab(const float4 *x, const DRay &r, float &tmin_o, float &tmax_o) {
+    const f3 O = tpos_rows(x[0], x[1], x[2], r.O), D = tvec_rows(x[0], x[1], x[2], r.D);
+    const float4 d0 = x[6], d1 = x[7];
+    const float rDx = 1 / D.x, rDy = 1 / D.y, rDz = 1 / D.z;
+    const bool sx = D.x < 0, sy = D.y < 0, sz = D.z < 0;
+    float tmin = ((sx ? d1.x : d0.x) - O.x) * rDx;
+    float tmax = ((sx ? d0.x : d1.x) - O.x) * rDx;
+    const float tymin = ((sy ? d1.y : d0.y) - O.y) * rDy;
+    const float tymax = ((sy ? d0.y : d1.y) - O.y) * rDy;
+    if (tmin > tymax || tymin > tmax) return false;
+    tmin = smax(tmin, tymin);
+    tmax = smin(tmax, tymax);
+    const float tzmin = ((sz ? d1.z : d0.z) - O.z) * rDz;
+    const float tzmax = ((sz ? d0.z : d1.z) - O.z) * rDz;
+    if (tmin > tzmax || tzmin > tmax) return false;
+    tmin_o = smax(tmin, tzmin);
+    tmax_o = smin(tmax, tzmax);
+    return true;
+}
+// QUAD plane distance in object space (Primitive.h:111-117 / 236-247)
+__device__ __forceinline__ float quad_t(const float4 *x, const DRay &r, f3 &O, f3 &D) {
+    O = tpos_rows(x[0], x[1], x[2], r.O);
+    D = tvec_rows(x[0], x[1], x[2], r.D);
+    return O.y / -D.y;
+}
+// cubes and quads (off the hot path): Intersect; `tie` as in prim_intersect_t
+__device__ __noinline__ void xprim_intersect(const SceneView &S, uint32_t type, uint32_t xi, int id, DRay &r,
+                                             bool &tie) {
+    const float4 *x = S.xprims + 8 * xi;
+    if (type == T_CUBE) {   // the acceptance test is on tmax (Primitive.h:221-233)
+        float tmin, tmax;
+        if (!cube_slab(x, r, tmin, tmax)) return;
+        float t;
+        if (tmin > kEPS) t = tmin;
+        else if (tmax > kEPS) t = tmax;
+        else return;
+        if (tmax < r.t) { r.t = t; r.obj = id; }
+        else if (tmax == r.t) tie = true;
+    } else {
+        f3 O, D;
+        const float t = quad_t(x, r, O, D);
+        const float size = x[6].x;
+        if (t <= r.t && t > kEPS) {
+            const f3 I = O + t * D;
+            if (I.x > -size && I.x < size && I.z > -size && I.z < size) {
+                if (t == r.t) tie = true;
+                else { r.t = t; r.obj = id; r.u = 0.0f; r.v = 0.0f; }   // u, v unset there: 0
+            }
+        }
+    }
+}
+__device__ __noinline__ bool xprim_hit(const SceneView &S, uint32_t type, uint32_t xi, const DRay &r) {
+    const float4 *x = S.xprims + 8 * xi;
+    if (type == T_CUBE) {
+        float tmin, tmax;
+        if (!cube_slab(x, r, tmin, tmax)) return false;
+        return (tmin > kEPS || tmax > kEPS) && tmax < r.t;
+    }
+    f3 O, D;
+    const float t = quad_t(x, r, O, D);   // the quad's extent is not tested (reference quirk)
+    return t < r.t && t > kEPS;
+}
 __device__ __forceinline__ void prim_intersect(const SceneView &S, uint32_t k, DRay &r) {
     float4 p0 = S.prims[3 * k], p1 = S.prims[3 * k + 1];
     uint32_t type = __float_as_uint(p1.w);
@@ -169,10 +248,13 @@ __device__ __forceinline__ void prim_intersect(const SceneView &S, uint32_t k, D
             if (!(t < r.t && t > kEPS)) return;
         }
         r.t = t; r.obj = id;            // u, v filled in after traversal (finish_uv)
-    } else {
+    } else if (type == T_PLANE) {
         f3 N = mk(p0.x, p0.y, p0.z);
         float t = -(dot(r.O, N) + p1.x) / (dot(r.D, N));
         if (t < r.t && t > kEPS) { r.t = t; r.obj = id; }
+    } else {
+        bool tie = false;
+        xprim_intersect(S, type, __float_as_uint(p1.x), id, r, tie);
     }
 }
 
@@ -212,11 +294,13 @@ __device__ __forceinline__ void prim_intersect_t(const SceneView &S, uint32_t k,
             if (!(t < r.t && t > kEPS)) return;
         }
         r.t = t; r.obj = id;
-    } else {
+    } else if (type == T_PLANE) {
         f3 N = mk(p0.x, p0.y, p0.z);
         float t = -(dot(r.O, N) + p1.x) / (dot(r.D, N));
         if (t == r.t && t > kEPS) tie = true;
         if (t < r.t && t > kEPS) { r.t = t; r.obj = id; }
+    } else {
+        xprim_intersect(S, type, __float_as_uint(p1.x), id, r, tie);
     }
 }
 
@@ -246,10 +330,12 @@ __device__ __forceinline__ bool prim_hit(const SceneView &S, uint32_t k, const D
         if (t < r.t && t > kEPS) return true;
         t = d - b;
         return t < r.t && t > kEPS;
-    } else {
+    } else if (type == T_PLANE) {
         f3 N = mk(p0.x, p0.y, p0.z);
         float t = -(dot(r.O, N) + p1.x) / (dot(r.D, N));
         return t < r.t && t > kEPS;
+    } else {
+        return xprim_hit(S, type, __float_as_uint(p1.x), r);
     }
 }
 
@@ -268,7 +354,64 @@ __device__ __forceinline__ void finish_uv(const SceneView &S, DRay &r) {
         if (s0.x < kFLT_EPSILON && s0.y < kFLT_EPSILON) { r.u = I.x; r.v = -I.y; }
         else if (s0.x < kFLT_EPSILON && s0.z < kFLT_EPSILON) { r.u = I.x; r.v = -I.z; }
         else if (s0.y < kFLT_EPSILON && s0.z < kFLT_EPSILON) { r.u = I.y; r.v = -I.z; }
+        else { r.u = 0.0f; r.v = 0.0f; }   // left unset by the reference: defined as 0
+    } else if (type == T_QUAD) {
+        r.u = 0.0f; r.v = 0.0f;
+    } else if (type == T_CUBE) {           // Primitive::setTextureCoordsCube, Primitive.h:752-797
+        const float4 *x = S.xprims + 8 * __float_as_uint(s1.z);
+        const f3 o = tpos_rows(x[0], x[1], x[2], I);
+        const float4 d0 = x[6], d1 = x[7];
+        float uc = o.z, vc = o.y;
+        const float e0 = fabsf(o.x - d0.x), e1 = fabsf(o.x - d1.x), e2 = fabsf(o.y - d0.y), e3 = fabsf(o.y - d1.y);
+        const float e4 = fabsf(o.z - d0.z), e5 = fabsf(o.z - d1.z);
+        float minDist = e0;
+        int face = 1;
+        if (e1 < minDist) uc = -o.z, vc = o.y, face = 0, minDist = e1;
+        if (e2 < minDist) uc = o.x, vc = o.z, face = 3, minDist = e2;
+        if (e3 < minDist) uc = o.x, vc = -o.z, face = 2, minDist = e3;
+        if (e4 < minDist) uc = -o.x, vc = o.y, face = 5, minDist = e4;
+        if (e5 < minDist) uc = o.x, vc = o.y, face = 4;
+        uc = -uc, vc = -vc;
+        uc = 0.5f * (uc / d1.x + 1.0f);
+        vc = 0.5f * (vc / d1.x + 1.0f);
+        const float third = 1.0f / 3.0f;
+        const float fu = face == 0 ? 2.0f : face == 1 ? 0.0f : face == 5 ? 3.0f : 1.0f;
+        const float fv = face == 2 ? 0.0f : face == 3 ? 2.0f : 1.0f;
+        r.u = 0.25f * (fu + uc);
+        r.v = third * (fv + vc);
     }
+}
+
+// Scene::GetNormal (template/scene.h:489-497) of the hit primitive at I, not yet flipped:
+// Primitive::GetNormal (Primitive.h:284-314)
+__device__ __forceinline__ f3 prim_normal(const SceneView &S, int obj, f3 I) {
+    const float4 s0 = S.shade[2 * obj], s1 = S.shade[2 * obj + 1];
+    const uint32_t type = __float_as_uint(s1.x);
+    if (type == T_SPH) return (I - mk(s0.x, s0.y, s0.z)) * s1.y;
+    if (type != T_CUBE) return mk(s0.x, s0.y, s0.z);
+    const float4 *x = S.xprims + 8 * __float_as_uint(s1.z);
+    const f3 o = tpos_rows(x[0], x[1], x[2], I);
+    const float4 d0 = x[6], d1 = x[7];
+    f3 N = mk(-1, 0, 0);
+    const float e0 = fabsf(o.x - d0.x), e1 = fabsf(o.x - d1.x), e2 = fabsf(o.y - d0.y), e3 = fabsf(o.y - d1.y);
+    const float e4 = fabsf(o.z - d0.z), e5 = fabsf(o.z - d1.z);
+    float minDist = e0;
+    if (e1 < minDist) minDist = e1, N.x = 1;
+    if (e2 < minDist) minDist = e2, N = mk(0, -1, 0);
+    if (e3 < minDist) minDist = e3, N = mk(0, 1, 0);
+    if (e4 < minDist) minDist = e4, N = mk(0, 0, -1);
+    if (e5 < minDist) minDist = e5, N = mk(0, 0, 1);
+    return tvec_rows(x[3], x[4], x[5], N);
+}
+
+// Scene::GetNormal (flipped against the ray) and Scene::GetMaterial of a hit; a
+// TextureMaterial also needs the hit's u, v (deferred by the traversal, finish_uv)
+__device__ __forceinline__ const DevMaterial &hit_surface(const SceneView &S, DRay &ray, f3 I, f3 &N) {
+    N = prim_normal(S, ray.obj, I);
+    if (dot(N, ray.D) > 0) N = -N;
+    const DevMaterial &m = S.mats[__float_as_int(S.shade[2 * ray.obj].w)];
+    if (m.kind == RT_TEXTURE) finish_uv(S, ray);
+    return m;
 }
 
 // ------------------------------------------------------------------ traversal (scene.h:285-320, 452-487)
@@ -563,7 +706,16 @@ __device__ __forceinline__ bool scatter(const DevMaterial &m, const DRay &in, f3
     }
 }
 
-__device__ __forceinline__ f3 mat_color(const DevMaterial &m, const DRay &in, f3 I) {
+// TextureMaterial::GetColor (TextureMaterial.h:30-37); scale = 1/255 (correction) or
+// SKYDOME_CORRECTION (getColorModifier) -- the same float
+__device__ __forceinline__ f3 texture_color(const SceneView &S, const DevMaterial &m, const DRay &in) {
+    const uint32_t u = f2u_wrap((float)m.tex_w * in.u), v = f2u_wrap((float)m.tex_h * in.v);
+    const uint32_t p = S.tex[m.tex_off + (u & (m.tex_w - 1)) + (v & (m.tex_h - 1)) * m.tex_w];
+    return mk((float)((p >> 16) & 255), (float)((p >> 8) & 255), (float)(p & 255)) * (1.0f / 255.0f);
+}
+
+__device__ __forceinline__ f3 mat_color(const SceneView &S, const DevMaterial &m, const DRay &in, f3 I) {
+    if (m.kind == RT_TEXTURE) return texture_color(S, m, in);
     if (m.kind == RT_DIELECTRIC) {                                     // Dielectric.h:12-21
         f3 c = mk(1, 1, 1);
         if (in.inside) { c.x = exp_f(-m.c0[0] * in.t); c.y = exp_f(-m.c0[1] * in.t); c.z = exp_f(-m.c0[2] * in.t); }
@@ -577,8 +729,13 @@ __device__ __forceinline__ f3 mat_color(const DevMaterial &m, const DRay &in, f3
     return mk(m.c0[0], m.c0[1], m.c0[2]);
 }
 
-// Scene::GetLightPos = Primitive::GetRandomPoint of the light sphere (Primitive.h:394-402)
+// Scene::GetLightPos = Primitive::GetRandomPoint of the light (Primitive.h:394-402, 423-427)
 __device__ __forceinline__ f3 light_point(const SceneView &S, uint32_t &seed) {
+    if (S.light_quad) {   // Primitive.h:423-427: the point lies in object z = 0 (reference quirk)
+        const float a = S.light_qsize * (rnd_f(seed) - 1.0f);
+        const float b = S.light_qsize * (rnd_f(seed) - 1.0f);
+        return tpos(S.light_M, mk(a, b, 0.0f));
+    }
     f3 pt = mk(1, 1, 1);
     while (dot(pt, pt) > 1) {
         float x = rnd_f(seed) * 2.0f - 1.0f;
@@ -594,11 +751,12 @@ template <int STRIDE>
 __device__ __forceinline__ f3 nee(const SceneView &S, const Trav<STRIDE> &T, f3 I, f3 N, f3 BRDF, uint32_t &seed,
                                   uint32_t &nshadow) {
     f3 Il = light_point(S, seed);
-    float area = 4.0f * kPI * S.light_r2;                              // GetArea, Primitive.h:452
+    const float area = S.light_area;                                   // GetArea, Primitive.h:450-468
     f3 L = Il - I;
     float dist = length(L);
     L = L / dist;
-    f3 Nl = (Il - mk(S.light_c[0], S.light_c[1], S.light_c[2])) * S.light_invr;
+    f3 Nl = S.light_quad ? mk(S.light_N[0], S.light_N[1], S.light_N[2])
+                         : (Il - mk(S.light_c[0], S.light_c[1], S.light_c[2])) * S.light_invr;
     if (dot(Nl, L) > 0) Nl = -Nl;                                      // Scene::GetNormal flip
     float dotNL = dot(N, L), dotNlL = dot(Nl, -L);
     f3 Ld = mk(0, 0, 0);
@@ -608,8 +766,9 @@ __device__ __forceinline__ f3 nee(const SceneView &S, const Trav<STRIDE> &T, f3 
         if (!occluded(S, T, sh)) {
             float solid = (dotNlL * area) / (dist * dist);
             float lightPDF = 1.0f / solid;
-            const DevMaterial &lm = S.mats[S.light_mat];
-            Ld = (mk(lm.c0[0], lm.c0[1], lm.c0[2]) * BRDF) * (dotNL / lightPDF);
+            const DevMaterial &lm = S.mats[S.light_mat];                // GetLightColor(0, toLight)
+            const f3 lc = lm.kind == RT_LIGHT ? mk(lm.c0[0], lm.c0[1], lm.c0[2]) : mat_color(S, lm, sh, sh.O + sh.t * sh.D);
+            Ld = (lc * BRDF) * (dotNL / lightPDF);
         }
     }
     return Ld;
@@ -632,16 +791,13 @@ __device__ f3 trace_path(const SceneView &S, const Trav<STRIDE> &T, DRay ray, in
         else closest_hit(S, T, ray);
         if (ray.obj == -1) { term = sky_color<TEX_SKY>(S, ray.D); break; }
         f3 I = ray.O + ray.t * ray.D;
-        float4 s0 = S.shade[2 * ray.obj], s1 = S.shade[2 * ray.obj + 1];
-        uint32_t ptype = __float_as_uint(s1.x);
-        f3 N = ptype == T_SPH ? (I - mk(s0.x, s0.y, s0.z)) * s1.y : mk(s0.x, s0.y, s0.z);
-        if (dot(N, ray.D) > 0) N = -N;                                 // Scene::GetNormal
-        const DevMaterial &m = S.mats[__float_as_int(s0.w)];
+        f3 N;
+        const DevMaterial &m = hit_surface(S, ray, I, N);
         if (m.flag == F_LIGHT) { term = lastSpec ? mk(m.c0[0], m.c0[1], m.c0[2]) : mk(0, 0, 0); break; }
         const bool last = MAXD == 1 || d == 1;   // MAXD 1: the bounce ray is never traced
         DRay out;
         bool spec = scatter(m, ray, I, N, out, seed, last);
-        f3 albedo = mat_color(m, ray, I);
+        f3 albedo = mat_color(S, m, ray, I);
         if (m.flag == F_DIFFUSE || (m.flag == F_MIX && !spec)) {
             f3 BRDF = albedo * kINVPI;
             lv_add[levels] = nee(S, T, I, N, BRDF, seed, nshadow);
@@ -668,18 +824,16 @@ __device__ f3 trace_path(const SceneView &S, const Trav<STRIDE> &T, DRay ray, in
 // Renderer::TracePacket's per-ray shading (renderer.cpp:78-133): the primary hit comes
 // from the packet traversal, every bounce is a Trace(ray_out, specularBounce, depth).
 template <int MAXD, bool TEX_SKY, int STRIDE>
-__device__ f3 shade_packet(const SceneView &S, const Trav<STRIDE> &T, const DRay &ray, int depth, uint32_t &seed,
+__device__ f3 shade_packet(const SceneView &S, const Trav<STRIDE> &T, DRay ray, int depth, uint32_t &seed,
                            uint32_t &nshadow, uint32_t &nbounce) {
     if (ray.obj == -1) return sky_color<TEX_SKY>(S, ray.D);
     f3 I = ray.O + ray.t * ray.D;
-    float4 s0 = S.shade[2 * ray.obj], s1 = S.shade[2 * ray.obj + 1];
-    f3 N = __float_as_uint(s1.x) == T_SPH ? (I - mk(s0.x, s0.y, s0.z)) * s1.y : mk(s0.x, s0.y, s0.z);
-    if (dot(N, ray.D) > 0) N = -N;                                     // Scene::GetNormal
-    const DevMaterial &m = S.mats[__float_as_int(s0.w)];
+    f3 N;
+    const DevMaterial &m = hit_surface(S, ray, I, N);
     const bool last = depth == 0;                  // Trace(.., 0) returns 0: the bounce is never traced
     DRay out;
     bool spec = scatter(m, ray, I, N, out, seed, last);
-    f3 albedo = mat_color(m, ray, I);
+    f3 albedo = mat_color(S, m, ray, I);
     if (m.flag == F_LIGHT) return albedo;
     const bool diffuse = m.flag == F_DIFFUSE || m.flag == F_MIX;
     // MIX + specular bounce: the ray is traced for a result that is then overwritten
@@ -701,7 +855,7 @@ __device__ f3 shade_packet(const SceneView &S, const Trav<STRIDE> &T, const DRay
 // ObjectMaterial::getColorModifier overrides: colour in c, colorVars[3] in c3 and the
 // refraction direction colorVars[4..6] in T (Diffuse.h:21-23, Mirror.h:21-23,
 // Light.h:20-22, Checkerboard.h:60-71, Dielectric.h:56-85).
-__device__ __forceinline__ void color_modifier(const DevMaterial &m, const DRay &in, f3 I, f3 N, f3 &c, float &c3,
+__device__ __forceinline__ void color_modifier(const SceneView &S, const DevMaterial &m, const DRay &in, f3 I, f3 N, f3 &c, float &c3,
                                                f3 &T) {
     c3 = 0.0f;
     T = mk(0, 0, 0);
@@ -710,7 +864,12 @@ __device__ __forceinline__ void color_modifier(const DevMaterial &m, const DRay 
         c = mk(fmaxf(0.0f, fminf(m.c0[0], 1.0f)), fmaxf(0.0f, fminf(m.c0[1], 1.0f)), fmaxf(0.0f, fminf(m.c0[2], 1.0f)));
         return;
     case RT_CHECKERBOARD:
-        c = mat_color(m, in, I);
+    case RT_TEXTURE:                 // TextureMaterial.h:62-71
+        c = mat_color(S, m, in, I);
+        c3 = m.diffuse;
+        return;
+    case RT_DSMIX:                   // DSMix.h:48-50
+        c = mk(m.c0[0], m.c0[1], m.c0[2]);
         c3 = m.diffuse;
         return;
     case RT_DIELECTRIC: {
@@ -788,13 +947,11 @@ __device__ f3 trace_whitted(const SceneView &S, const Trav<STRIDE> &T, DRay ray,
                 ret = sky_color<TEX_SKY>(S, ray.D);
             } else {
                 f3 I = ray.O + ray.t * ray.D;
-                float4 s0 = S.shade[2 * ray.obj], s1 = S.shade[2 * ray.obj + 1];
-                f3 N = __float_as_uint(s1.x) == T_SPH ? (I - mk(s0.x, s0.y, s0.z)) * s1.y : mk(s0.x, s0.y, s0.z);
-                if (dot(N, ray.D) > 0) N = -N;                         // Scene::GetNormal
-                const DevMaterial &m = S.mats[__float_as_int(s0.w)];
+                f3 N;
+                const DevMaterial &m = hit_surface(S, ray, I, N);
                 f3 col, Tdir;
                 float c3;
-                color_modifier(m, ray, I, N, col, c3, Tdir);
+                color_modifier(S, m, ray, I, N, col, c3, Tdir);
                 f3 res = mk(0, 0, 0);
                 WFrame f;
                 f.col = col; f.w = 1.0f; f.ft = 0.0f; f.flags = 0;
@@ -1057,7 +1214,9 @@ struct rt_scene {
     uint32_t stack_depth = 0;   // LDS stack entries per lane
     bool lds_nodes = false;     // frame kernel keeps the node array in LDS (k_render_lds)
     uint32_t num_cus = 256;     // persistent grid size of k_render_lds
+    bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
+    void *d_xprims = nullptr, *d_tex = nullptr;
     void *d_scratch = nullptr;  // staging for the host-pointer batched calls
     size_t scratch_bytes = 0;
     hipStream_t stream = nullptr;
@@ -1127,7 +1286,7 @@ void free_scene(rt_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     (void)hipDeviceSynchronize();
-    void *ptrs[] = {s->d_nodes, s->d_prims, s->d_shade, s->d_mats, s->d_sky, s->d_scratch};
+    void *ptrs[] = {s->d_nodes, s->d_prims, s->d_shade, s->d_mats, s->d_sky, s->d_xprims, s->d_tex, s->d_scratch};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -1150,6 +1309,11 @@ int ensure_device(int device) {
     return RT_OK;
 }
 
+inline f3 tvec_host(float4 r0, float4 r1, float4 r2, f3 a) {
+    const float M[12] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w};
+    return tvec(M, a);
+}
+
 int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (!d || !out || !d->prims || d->num_prims == 0 || !d->materials || d->num_materials == 0)
         return fail(RT_ERR_INVALID, "rt_scene_create: empty or null description");
@@ -1158,13 +1322,22 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (n >= (1u << 24)) return fail(RT_ERR_UNSUPPORTED, "more than 2^24 primitives");
     for (uint32_t i = 0; i < n; ++i) {
         const rt_prim &p = d->prims[i];
-        if (p.type != RT_SPHERE && p.type != RT_PLANE && p.type != RT_TRIANGLE)
+        if (p.type < RT_SPHERE || p.type > RT_TRIANGLE)
             return fail(RT_ERR_INVALID, "primitive " + std::to_string(i) + ": unknown type");
         if (p.material < 0 || (uint32_t)p.material >= d->num_materials)
             return fail(RT_ERR_INVALID, "primitive " + std::to_string(i) + ": material out of range");
     }
-    if (d->prims[0].type != RT_SPHERE)
-        return fail(RT_ERR_UNSUPPORTED, "primitive 0 must be the light sphere (Scene::GetRandomLight returns 0)");
+    if (d->prims[0].type != RT_SPHERE && d->prims[0].type != RT_QUAD)
+        return fail(RT_ERR_UNSUPPORTED, "primitive 0 must be the light, a sphere or a quad (Scene::GetRandomLight returns 0)");
+    for (uint32_t i = 0; i < d->num_materials; ++i) {
+        const rt_material &m = d->materials[i];
+        if (m.kind < RT_DIFFUSE || m.kind > RT_TEXTURE) return fail(RT_ERR_INVALID, "unknown material kind");
+        if (m.kind == RT_TEXTURE && (m.texture < 0 || (uint32_t)m.texture >= d->num_textures || !d->textures))
+            return fail(RT_ERR_INVALID, "material " + std::to_string(i) + ": texture index out of range");
+    }
+    for (uint32_t i = 0; i < d->num_textures; ++i)
+        if (!d->textures[i].pixels || !d->textures[i].width || !d->textures[i].height)
+            return fail(RT_ERR_INVALID, "texture " + std::to_string(i) + " is empty");
     if (d->sky_pixels) {
         uint32_t w = d->sky_width, h = d->sky_height;
         if (!w || !h || (w & (w - 1)) || (h & (h - 1)))
@@ -1199,7 +1372,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
             st.push_back({nd.leftFirst, dd + 1});
             st.push_back({nd.leftFirst + 1, dd + 1});
         }
-    } else if ((rc = build_bvh(d->prims, n, s->bvh)) != RT_OK) {
+    } else if ((rc = build_bvh(d->prims, d->transforms, n, s->bvh)) != RT_OK) {
         delete s;
         return rc;
     }
@@ -1215,13 +1388,39 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         nodes[2 * i] = make_float4(nd.mn[0], nd.mn[1], nd.mn[2], nd.mx[0]);
         nodes[2 * i + 1] = make_float4(nd.mx[1], nd.mx[2], ubits(word), 0.0f);
     }
-    // ---- leaf-order primitive records and per-id shading records
+    // ---- leaf-order primitive records and per-id shading records; cubes and quads keep
+    // their matrices and data in a side table (8 float4 each)
     static const float I16[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-    std::vector<float4> prims(3 * (size_t)n), shade(2 * (size_t)n);
+    std::vector<float4> prims(3 * (size_t)n), shade(2 * (size_t)n), xprims;
+    std::vector<uint32_t> xindex(n, 0);
+    for (uint32_t id = 0; id < n; ++id) {
+        const rt_prim &p = d->prims[id];
+        if (p.type != RT_CUBE && p.type != RT_QUAD) continue;
+        if (p.type == RT_CUBE) s->has_cubes = true;
+        PrimX x;
+        prim_transform(p, d->transforms ? d->transforms + 16 * (size_t)id : nullptr, x);
+        xindex[id] = (uint32_t)(xprims.size() / 8);
+        for (int r = 0; r < 3; ++r) xprims.push_back(make_float4(x.Minv[4 * r], x.Minv[4 * r + 1], x.Minv[4 * r + 2], x.Minv[4 * r + 3]));
+        for (int r = 0; r < 3; ++r) xprims.push_back(make_float4(x.M[4 * r], x.M[4 * r + 1], x.M[4 * r + 2], x.M[4 * r + 3]));
+        if (p.type == RT_CUBE) {   // data[0] = -0.5 size, data[1] = 0.5 size (Primitive.h:724-725)
+            const f3 sz = mk(p.v[3], p.v[4], p.v[5]), a = -0.5f * sz, b = 0.5f * sz;
+            xprims.push_back(make_float4(a.x, a.y, a.z, 0.0f));
+            xprims.push_back(make_float4(b.x, b.y, b.z, 0.0f));
+        } else {                   // data[0].x = 0.5 size (Primitive.h:737)
+            xprims.push_back(make_float4(0.5f * p.v[0], 0.0f, 0.0f, 0.0f));
+            xprims.push_back(make_float4(0, 0, 0, 0));
+        }
+    }
     for (uint32_t id = 0; id < n; ++id) {
         const rt_prim &p = d->prims[id];
         float4 s0, s1 = make_float4(ubits((uint32_t)p.type), 0, 0, 0);
-        if (p.type == RT_TRIANGLE) {
+        if (p.type == RT_CUBE || p.type == RT_QUAD) {
+            const float4 *x = &xprims[8 * (size_t)xindex[id]];
+            // quad: constant normal TransformVector((0,-1,0), Transform) (Primitive.h:306-307)
+            f3 N = p.type == RT_QUAD ? tvec_host(x[3], x[4], x[5], mk(0, -1, 0)) : mk(0, 0, 0);
+            s0 = make_float4(N.x, N.y, N.z, ibits(p.material));
+            s1.z = ubits(xindex[id]);
+        } else if (p.type == RT_TRIANGLE) {
             f3 d0 = mk(p.v[0], p.v[1], p.v[2]), d1 = mk(p.v[3], p.v[4], p.v[5]), d2 = mk(p.v[6], p.v[7], p.v[8]);
             f3 N = tvec(I16, normalize(cross(d2 - d0, d1 - d0)));      // Primitive.h:308-310
             s0 = make_float4(N.x, N.y, N.z, ibits(p.material));
@@ -1257,12 +1456,25 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
             q[0] = make_float4(c.x, c.y, c.z, ibits((int)id));
             q[1] = make_float4(r * r, 0.0f, 0.0f, ubits(T_SPH)); // data[0].y
             q[2] = make_float4(0, 0, 0, 0);
-        } else {
+        } else if (p.type == RT_PLANE) {
             q[0] = make_float4(p.v[0], p.v[1], p.v[2], ibits((int)id));
             q[1] = make_float4(p.v[3], 0.0f, 0.0f, ubits(T_PLANE));
             q[2] = make_float4(0, 0, 0, 0);
+        } else {
+            q[0] = make_float4(0, 0, 0, ibits((int)id));
+            q[1] = make_float4(ubits(xindex[id]), 0.0f, 0.0f, ubits(p.type == RT_CUBE ? T_CUBE : T_QUAD));
+            q[2] = make_float4(0, 0, 0, 0);
         }
     }
+    // ---- textures, concatenated
+    std::vector<uint32_t> texels, tex_offsets;
+    for (uint32_t i = 0; i < d->num_textures; ++i) {
+        const rt_texture &t = d->textures[i];
+        tex_offsets.push_back((uint32_t)texels.size());
+        texels.insert(texels.end(), t.pixels, t.pixels + (size_t)t.width * t.height);
+    }
+    if (texels.empty()) texels.push_back(0);
+    if (xprims.empty()) xprims.push_back(make_float4(0, 0, 0, 0));
     // ---- materials
     std::vector<DevMaterial> mats(d->num_materials);
     for (uint32_t i = 0; i < d->num_materials; ++i) {
@@ -1270,12 +1482,18 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         DevMaterial &o = mats[i];
         std::memset(&o, 0, sizeof(o));
         o.kind = m.kind;
-        if (m.kind < RT_DIFFUSE || m.kind > RT_LIGHT) { delete s; return fail(RT_ERR_INVALID, "unknown material kind"); }
         for (int c = 0; c < 3; ++c) { o.c0[c] = m.color[c]; o.c1[c] = m.color2[c]; }
         o.ior = m.ior;
-        if (m.kind == RT_CHECKERBOARD) {   // Checkerboard.h:6-14
-            if (m.diffuse < 0.0f) { o.diffuse = 1.0f; o.specular = 0.0f; }
+        // Checkerboard.h:6-14, TextureMaterial.h:6-17 (short ctor: diffuse 1, specular 0),
+        // DSMix.h:6-9 (always clamped): clamp = fmaxf(a, fminf(f, b)), precomp.h:782
+        if (m.kind == RT_CHECKERBOARD || m.kind == RT_TEXTURE || m.kind == RT_DSMIX) {
+            if (m.diffuse < 0.0f && m.kind != RT_DSMIX) { o.diffuse = 1.0f; o.specular = 0.0f; }
             else { o.diffuse = tmax(0.0f, tmin(m.diffuse, 1.0f)); o.specular = 1.0f - o.diffuse; }
+        }
+        if (m.kind == RT_TEXTURE) {
+            const rt_texture &t = d->textures[m.texture];
+            o.tex_off = tex_offsets[m.texture];
+            o.tex_w = t.width; o.tex_h = t.height;
         }
         o.flag = material_flag(m, o.diffuse, o.specular);
     }
@@ -1296,6 +1514,8 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (rc == RT_OK) rc = upload(&s->d_shade, shade);
     if (rc == RT_OK) rc = upload(&s->d_mats, mats);
     if (rc == RT_OK) rc = upload(&s->d_sky, sky);
+    if (rc == RT_OK) rc = upload(&s->d_xprims, xprims);
+    if (rc == RT_OK) rc = upload(&s->d_tex, texels);
     if (rc == RT_OK && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(RT_ERR_HIP, "hipStreamCreate failed");
     if (rc != RT_OK) { free_scene(s); return rc; }
@@ -1306,6 +1526,8 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     v.shade = (const float4 *)s->d_shade;
     v.mats = (const DevMaterial *)s->d_mats;
     v.sky = (const uint32_t *)s->d_sky;
+    v.xprims = (const float4 *)s->d_xprims;
+    v.tex = (const uint32_t *)s->d_tex;
     v.sky_w = sw; v.sky_h = sh;
     v.sky_const = sky_const ? 1 : 0;
     {
@@ -1314,15 +1536,25 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         v.sky_rgb[0] = c.x; v.sky_rgb[1] = c.y; v.sky_rgb[2] = c.z;
     }
     const rt_prim &L = d->prims[0];
-    float T[16];
-    translate_matrix(L.v[0], L.v[1], L.v[2], T);
-    std::memcpy(v.light_M, T, sizeof(v.light_M));
-    f3 lc = tpos(T, mk(0, 0, 0));
+    PrimX LX;
+    prim_transform(L, d->transforms ? d->transforms : nullptr, LX);
+    std::memcpy(v.light_M, LX.M, sizeof(v.light_M));
+    f3 lc = tpos(LX.M, mk(0, 0, 0));
     v.light_c[0] = lc.x; v.light_c[1] = lc.y; v.light_c[2] = lc.z;
-    v.light_r = L.v[3];
-    v.light_r2 = L.v[3] * L.v[3];
-    v.light_invr = 1.0f / L.v[3];
     v.light_mat = L.material;
+    v.light_quad = L.type == RT_QUAD;
+    if (v.light_quad) {
+        v.light_qsize = 0.5f * L.v[0];
+        const float side = 2.0f * v.light_qsize;                      // GetArea, Primitive.h:461-463
+        v.light_area = side * side;
+        const f3 N = tvec(LX.M, mk(0, -1, 0));
+        v.light_N[0] = N.x; v.light_N[1] = N.y; v.light_N[2] = N.z;
+    } else {
+        v.light_r = L.v[3];
+        v.light_r2 = L.v[3] * L.v[3];
+        v.light_invr = 1.0f / L.v[3];
+        v.light_area = 4.0f * kPI * v.light_r2;                        // Primitive.h:452
+    }
     const Node &root = s->bvh.nodes[0];
     v.root_word = (root.leftFirst << 8) | root.count;
     {
@@ -1337,7 +1569,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 #endif
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
     v.wave_primary = 0;
-    if (const char *e = std::getenv("RT_WAVE_PRIMARY")) v.wave_primary = std::atoi(e) != 0;
+    if (const char *e = std::getenv("RT_WAVE_PRIMARY")) v.wave_primary = std::atoi(e) != 0 && !s->has_cubes;
     v.bounds_finite = 1;
     for (uint32_t i = 0; i < s->bvh.nodes_used && v.bounds_finite; ++i) {
         if (i == 1) continue;
@@ -1501,6 +1733,8 @@ int rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
 int rt_scene_set_camera_walk(rt_scene *s, int walk) {
     if (!s) return fail(RT_ERR_INVALID, "null argument");
     if (walk != RT_WALK_LANE && walk != RT_WALK_WAVE) return fail(RT_ERR_INVALID, "unknown camera walk");
+    if (walk == RT_WALK_WAVE && s->has_cubes)
+        return fail(RT_ERR_UNSUPPORTED, "the wave walk needs order-independent hits; cubes accept on tmax (Primitive.h:221-233)");
     s->view.wave_primary = walk == RT_WALK_WAVE;
     return RT_OK;
 }

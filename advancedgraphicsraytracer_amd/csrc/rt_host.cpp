@@ -13,8 +13,11 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <iterator>
 #include <string>
 #include <vector>
+
+#include <zlib.h>
 
 #include "rt_internal.h"
 
@@ -166,11 +169,68 @@ struct Reader {
 }  // namespace obj
 
 // ------------------------------------------------------------------ primitive geometry
-void prim_geometry(const rt_prim &p, PrimGeom &g) {
+void fast_inverse(const float *c, float *r) {
+    std::memcpy(r, kIdentity, sizeof(kIdentity));
+    r[0] = c[0], r[1] = c[4], r[2] = c[8];
+    r[4] = c[1], r[5] = c[5], r[6] = c[9];
+    r[8] = c[2], r[9] = c[6], r[10] = c[10];
+    r[3] = -(c[3] * r[0] + c[7] * r[1] + c[11] * r[2]);
+    r[7] = -(c[3] * r[4] + c[7] * r[5] + c[11] * r[6]);
+    r[11] = -(c[3] * r[8] + c[7] * r[9] + c[11] * r[10]);
+}
+
+void prim_transform(const rt_prim &p, const float *T16, PrimX &x) {
+    const float *T = T16 ? T16 : kIdentity;
     if (p.type == RT_SPHERE) {
-        float T[16];
-        translate_matrix(p.v[0], p.v[1], p.v[2], T);
-        f3 c = tpos(T, mk(0, 0, 0));
+        translate_matrix(p.v[0], p.v[1], p.v[2], x.M);           // createSphere, Primitive.h:690-698
+    } else if (p.type == RT_CUBE) {                               // createCube, Primitive.h:717-728
+        const f3 pos = mk(p.v[0], p.v[1], p.v[2]);
+        if (length(pos) > kFLT_EPSILON) {
+            float Tr[16];
+            translate_matrix(pos.x, pos.y, pos.z, Tr);
+            mat_mul(T, Tr, x.M);
+        } else {
+            std::memcpy(x.M, T, sizeof(x.M));
+        }
+    } else if (p.type == RT_QUAD) {
+        std::memcpy(x.M, T, sizeof(x.M));
+    } else {
+        std::memcpy(x.M, kIdentity, sizeof(x.M));
+    }
+    fast_inverse(x.M, x.Minv);
+}
+
+// the 8 cube corners / 4 quad corners in GetAABBMin/Max's order (Primitive.h:325-341)
+static int box_corners(const rt_prim &p, const PrimX &x, f3 *c) {
+    if (p.type == RT_CUBE) {
+        const f3 a = -0.5f * mk(p.v[3], p.v[4], p.v[5]), b = 0.5f * mk(p.v[3], p.v[4], p.v[5]);
+        c[0] = tpos(x.M, a);
+        c[1] = tpos(x.M, mk(b.x, a.y, a.z));
+        c[2] = tpos(x.M, mk(a.x, b.y, a.z));
+        c[3] = tpos(x.M, mk(a.x, a.y, b.z));
+        c[4] = tpos(x.M, b);
+        c[5] = tpos(x.M, mk(a.x, b.y, b.z));
+        c[6] = tpos(x.M, mk(b.x, a.y, b.z));
+        c[7] = tpos(x.M, mk(b.x, b.y, a.z));
+        return 8;
+    }
+    const float sz = 0.5f * p.v[0];
+    c[0] = tpos(x.M, mk(-sz, 0, -sz));
+    c[1] = tpos(x.M, mk(-sz, 0, sz));
+    c[2] = tpos(x.M, mk(sz, 0, -sz));
+    c[3] = tpos(x.M, mk(sz, 0, sz));
+    return 4;
+}
+
+void prim_geometry(const rt_prim &p, const PrimX &x, PrimGeom &g) {
+    if (p.type == RT_CUBE || p.type == RT_QUAD) {
+        f3 c[8];
+        const int n = box_corners(p, x, c);
+        g.centroid = tpos(x.M, mk(0, 0, 0));                      // ctor leaves centroid 0
+        g.bmin = g.bmax = c[0];
+        for (int i = 1; i < n; ++i) { g.bmin = fmin3(g.bmin, c[i]); g.bmax = fmax3(g.bmax, c[i]); }
+    } else if (p.type == RT_SPHERE) {
+        f3 c = tpos(x.M, mk(0, 0, 0));
         float r = p.v[3];
         g.centroid = c;                       // centroid float3(0) through Transform
         g.bmin = c - mk(r, r, r);
@@ -325,10 +385,14 @@ class Builder {
 };
 }  // namespace
 
-int build_bvh(const rt_prim *prims, uint32_t n, Bvh &out) {
+int build_bvh(const rt_prim *prims, const float *transforms, uint32_t n, Bvh &out) {
     if (n == 0) return fail(RT_ERR_INVALID, "scene has no primitives");
     std::vector<PrimGeom> geo(n);
-    for (uint32_t i = 0; i < n; ++i) prim_geometry(prims[i], geo[i]);
+    for (uint32_t i = 0; i < n; ++i) {
+        PrimX x;
+        prim_transform(prims[i], transforms ? transforms + 16 * (size_t)i : nullptr, x);
+        prim_geometry(prims[i], x, geo[i]);
+    }
     Builder(geo, out).run(n);
     return RT_OK;
 }
@@ -499,6 +563,131 @@ int rt_obj_load(const char *path, float **verts, uint32_t *nv, int32_t **faces, 
     return RT_OK;
 }
 
+// ------------------------------------------------------------------ PNG (Surface::LoadImage)
+namespace png {
+inline uint32_t be32(const uint8_t *p) { return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | p[3]; }
+inline int paeth(int a, int b, int c) {
+    int p = a + b - c, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - c);
+    return (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+}
+// decode to 8-bit channels the way stbi_load(.., req_comp 0) reports them: grey 1, grey+alpha 2,
+// RGB 3, RGBA 4, palette 3 (4 with tRNS); 16-bit samples keep their high byte, 1/2/4-bit grey
+// is scaled to 0..255
+int decode(const std::vector<uint8_t> &f, std::vector<uint8_t> &out, uint32_t &W, uint32_t &H, int &n) {
+    static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+    if (f.size() < 8 || std::memcmp(f.data(), sig, 8) != 0) return fail(RT_ERR_IO, "not a PNG file");
+    size_t i = 8;
+    int depth = 0, ctype = -1, interlace = 0;
+    std::vector<uint8_t> idat, plte;
+    bool trns = false;
+    while (i + 8 <= f.size()) {
+        const uint32_t len = be32(&f[i]);
+        const uint8_t *type = &f[i + 4];
+        if (i + 12 + (size_t)len > f.size()) return fail(RT_ERR_IO, "truncated PNG chunk");
+        const uint8_t *d = &f[i + 8];
+        if (!std::memcmp(type, "IHDR", 4)) {
+            if (len < 13) return fail(RT_ERR_IO, "bad IHDR");
+            W = be32(d); H = be32(d + 4); depth = d[8]; ctype = d[9]; interlace = d[12];
+        } else if (!std::memcmp(type, "PLTE", 4)) {
+            plte.assign(d, d + len);
+        } else if (!std::memcmp(type, "tRNS", 4)) {
+            trns = true;
+        } else if (!std::memcmp(type, "IDAT", 4)) {
+            idat.insert(idat.end(), d, d + len);
+        } else if (!std::memcmp(type, "IEND", 4)) {
+            break;
+        }
+        i += 12 + (size_t)len;
+    }
+    if (ctype < 0 || !W || !H) return fail(RT_ERR_IO, "PNG without IHDR");
+    if (interlace) return fail(RT_ERR_UNSUPPORTED, "interlaced PNG");
+    int ch;
+    switch (ctype) {
+    case 0: ch = 1; break;
+    case 2: ch = 3; break;
+    case 3: ch = 1; break;
+    case 4: ch = 2; break;
+    case 6: ch = 4; break;
+    default: return fail(RT_ERR_IO, "bad PNG colour type");
+    }
+    if (!(depth == 8 || depth == 16 || ((ctype == 0 || ctype == 3) && (depth == 1 || depth == 2 || depth == 4))))
+        return fail(RT_ERR_UNSUPPORTED, "PNG bit depth");
+    if (ctype == 3 && plte.size() < 3) return fail(RT_ERR_IO, "palette PNG without PLTE");
+    const size_t bits = (size_t)W * ch * depth, stride = (bits + 7) / 8;
+    const size_t bpp = std::max<size_t>(1, (size_t)ch * depth / 8);
+    std::vector<uint8_t> raw((stride + 1) * H);
+    uLongf rawlen = (uLongf)raw.size();
+    if (uncompress(raw.data(), &rawlen, idat.data(), (uLong)idat.size()) != Z_OK || rawlen != raw.size())
+        return fail(RT_ERR_IO, "PNG image data does not inflate to the expected size");
+    std::vector<uint8_t> cur(stride), prev(stride, 0);
+    n = ctype == 3 ? (trns ? 4 : 3) : ch;
+    out.assign((size_t)W * H * n, 0);
+    for (uint32_t y = 0; y < H; ++y) {
+        const uint8_t *r = &raw[(stride + 1) * y];
+        const int ft = r[0];
+        for (size_t x = 0; x < stride; ++x) {
+            const int a = x >= bpp ? cur[x - bpp] : 0, b = prev[x], c = x >= bpp ? prev[x - bpp] : 0;
+            int v = r[1 + x];
+            switch (ft) {
+            case 0: break;
+            case 1: v += a; break;
+            case 2: v += b; break;
+            case 3: v += (a + b) >> 1; break;
+            case 4: v += paeth(a, b, c); break;
+            default: return fail(RT_ERR_IO, "bad PNG filter type");
+            }
+            cur[x] = (uint8_t)v;
+        }
+        uint8_t *o = &out[(size_t)W * n * y];
+        for (uint32_t x = 0; x < W; ++x) {
+            for (int k = 0; k < ch; ++k) {
+                int s;
+                if (depth == 16) s = cur[2 * ((size_t)x * ch + k)];
+                else if (depth == 8) s = cur[(size_t)x * ch + k];
+                else {   // 1/2/4-bit grey or palette index
+                    const size_t bit = (size_t)x * depth;
+                    s = (cur[bit >> 3] >> (8 - depth - (bit & 7))) & ((1 << depth) - 1);
+                    if (ctype == 0) s *= depth == 1 ? 0xff : depth == 2 ? 0x55 : 0x11;
+                }
+                if (ctype == 3) {
+                    if ((size_t)s * 3 + 2 >= plte.size()) return fail(RT_ERR_IO, "palette index out of range");
+                    o[(size_t)x * n + 0] = plte[3 * s]; o[(size_t)x * n + 1] = plte[3 * s + 1];
+                    o[(size_t)x * n + 2] = plte[3 * s + 2];
+                    if (n == 4) o[(size_t)x * n + 3] = 255;
+                } else {
+                    o[(size_t)x * n + k] = (uint8_t)s;
+                }
+            }
+        }
+        std::swap(cur, prev);
+    }
+    return RT_OK;
+}
+}  // namespace png
+
+int rt_image_load(const char *path, uint32_t **pixels, uint32_t *width, uint32_t *height) {
+    if (!path || !pixels || !width || !height) return fail(RT_ERR_INVALID, "rt_image_load: null argument");
+    std::ifstream in(path, std::ios::binary);
+    if (!in) return fail(RT_ERR_IO, std::string("File not found: ") + path);
+    std::vector<uint8_t> f((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+    std::vector<uint8_t> d;
+    uint32_t W = 0, H = 0;
+    int n = 0;
+    int rc = png::decode(f, d, W, H, n);
+    if (rc != RT_OK) return rc;
+    const size_t s = (size_t)W * H;
+    uint32_t *px = (uint32_t *)std::malloc(sizeof(uint32_t) * s);
+    if (!px) return fail(RT_ERR_INVALID, "out of memory");
+    if (n == 1) {                      // template/template.cpp:1587-1593
+        for (size_t i = 0; i < s; ++i) { const uint32_t p = d[i]; px[i] = p + (p << 8) + (p << 16); }
+    } else {                           // 1597: bytes i*n .. i*n+2 (past the end reads as 0)
+        auto at = [&](size_t k) -> uint32_t { return k < d.size() ? d[k] : 0u; };
+        for (size_t i = 0; i < s; ++i) px[i] = (at(i * n) << 16) + (at(i * n + 1) << 8) + at(i * n + 2);
+    }
+    *pixels = px; *width = W; *height = H;
+    return RT_OK;
+}
+
 int rt_mesh_load(const char *path, float **verts, uint32_t *nv, int32_t **faces, uint32_t *nt) {
     if (!path || !verts || !nv || !faces || !nt) return fail(RT_ERR_INVALID, "rt_mesh_load: null argument");
     std::vector<float> V;
@@ -578,10 +767,11 @@ int rt_recipe_describe(const char *name, const char *mesh_dir, rt_prim *prims, u
     return RT_OK;
 }
 
-int rt_bvh_build_host(const rt_prim *prims, uint32_t n, void *nodes, uint32_t *indices, rt_scene_info *info) {
+int rt_bvh_build_host(const rt_prim *prims, const float *transforms, uint32_t n, void *nodes, uint32_t *indices,
+                      rt_scene_info *info) {
     if (!prims || !nodes || !indices) return fail(RT_ERR_INVALID, "rt_bvh_build_host: null argument");
     Bvh b;
-    int rc = build_bvh(prims, n, b);
+    int rc = build_bvh(prims, transforms, n, b);
     if (rc != RT_OK) return rc;
     std::memcpy(nodes, b.nodes.data(), sizeof(Node) * b.nodes.size());
     std::memcpy(indices, b.indices.data(), sizeof(uint32_t) * n);

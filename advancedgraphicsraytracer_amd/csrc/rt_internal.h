@@ -19,10 +19,18 @@ struct Node {
 };
 static_assert(sizeof(Node) == 32, "BVHNode layout");
 
+// Primitive::Transform and InvertedTransform (Primitive.h:28-29, 39-41): Translate(centre)
+// for spheres, T * Translate(pos) (|pos| > FLT_EPSILON) or T for cubes, T for quads,
+// identity otherwise.  T16 = the caller's mat4 (NULL = identity).
+struct PrimX { float M[16], Minv[16]; };
+void prim_transform(const rt_prim &p, const float *T16, PrimX &x);
+// mat4::FastInvertedTransformNoScale (template/precomp.h:1061-1085)
+void fast_inverse(const float *M, float *out);
+
 // Per-primitive geometry the builder and the uploader need, evaluated exactly as
 // Primitive::GetCentroid / GetAABBMin / GetAABBMax (Primitive.h:42-50, 319-388, 443-445).
 struct PrimGeom { f3 centroid, bmin, bmax; };
-void prim_geometry(const rt_prim &p, PrimGeom &g);
+void prim_geometry(const rt_prim &p, const PrimX &x, PrimGeom &g);
 void translate_matrix(float x, float y, float z, float M[16]);
 
 // Plain binned-SAH BVH (template/scene.h:845-976).  nodes sized 2N+2, indices N.
@@ -31,7 +39,7 @@ struct Bvh {
     std::vector<uint32_t> indices;
     uint32_t nodes_used = 0, depth = 0, max_leaf = 0;
 };
-int build_bvh(const rt_prim *prims, uint32_t n, Bvh &out);
+int build_bvh(const rt_prim *prims, const float *transforms, uint32_t n, Bvh &out);
 
 // SURVEY.md 8(d) scenes as descriptions
 struct SceneSource {

@@ -20,7 +20,7 @@
  *     and synchronize it;
  *   - primitive ids follow creation order exactly as the reference's
  *     Primitive::objIdx (Primitive.h:37-38); the light is primitive 0 and must be a
- *     sphere (Scene::GetRandomLight, template/scene.h:225-227).
+ *     sphere or a quad (Scene::GetRandomLight, template/scene.h:225-227).
  * No CPU fallback exists: without a usable gfx950 device every compute entry
  * point fails with RT_ERR_NO_DEVICE.
  */
@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum {
     RT_OK = 0,
@@ -44,10 +44,12 @@ enum {
     RT_ERR_UNSUPPORTED = -5 /* scene outside the kernels' limits */
 };
 
-/* Primitive kinds, Primitive.h:8-14 (CUBE and QUAD are not on the hot path). */
-enum { RT_SPHERE = 0, RT_PLANE = 1, RT_TRIANGLE = 4 };
-/* Materials: Diffuse.h, Mirror.h, Dielectric.h, Checkerboard.h, Light.h. */
-enum { RT_DIFFUSE = 0, RT_MIRROR = 1, RT_DIELECTRIC = 2, RT_CHECKERBOARD = 3, RT_LIGHT = 4 };
+/* Primitive kinds, Primitive.h:8-14. */
+enum { RT_SPHERE = 0, RT_PLANE = 1, RT_CUBE = 2, RT_QUAD = 3, RT_TRIANGLE = 4 };
+/* Materials: Diffuse.h, Mirror.h, Dielectric.h, Checkerboard.h, Light.h, DSMix.h,
+ * TextureMaterial.h. */
+enum { RT_DIFFUSE = 0, RT_MIRROR = 1, RT_DIELECTRIC = 2, RT_CHECKERBOARD = 3, RT_LIGHT = 4, RT_DSMIX = 5,
+       RT_TEXTURE = 6 };
 /* Integrators behind Renderer::Tick (renderer.cpp:227-231; the K key toggles them,
  * renderer.h:138): Trace (path tracer, default depth 10, renderer.h:9), WhittedTrace
  * (default depth 20, renderer.h:13), and the PACKET_TRAVERSAL build of Tick
@@ -59,13 +61,24 @@ enum { RT_MODE_PATH = 0, RT_MODE_WHITTED = 1, RT_MODE_PACKET = 2 };
 /* One primitive, Primitive::create* factories (Primitive.h:690-747):
  *   RT_SPHERE:   v[0..2] centre, v[3] radius
  *   RT_PLANE:    v[0..2] normal, v[3] distance
- *   RT_TRIANGLE: v[0..8] three world-space vertices (post Scene::LoadModel) */
+ *   RT_CUBE:     v[0..2] position, v[3..5] size; createCube(pos, size, material, T)
+ *   RT_QUAD:     v[0] size; createQuad(size, material, T)
+ *   RT_TRIANGLE: v[0..8] three world-space vertices (post Scene::LoadModel)
+ * T (cube / quad only) comes from rt_scene_desc.transforms. */
 typedef struct { int32_t type; int32_t material; float v[9]; } rt_prim;
 
-/* One material.  color = Diffuse/Mirror/Light colour or Dielectric absorption;
- * color2 = Checkerboard second colour; ior = Dielectric n; diffuse = Checkerboard
- * diffuse share (< 0 selects the 2-argument constructor: diffuse 1, specular 0). */
-typedef struct { int32_t kind; float color[3]; float color2[3]; float ior; float diffuse; } rt_material;
+/* One material.  color = Diffuse/Mirror/Light/DSMix colour or Dielectric absorption;
+ * color2 = Checkerboard second colour; ior = Dielectric n; diffuse = the diffuse share
+ * of Checkerboard / DSMix / TextureMaterial (clamped to [0, 1]; < 0 selects the short
+ * Checkerboard / TextureMaterial constructor: diffuse 1, specular 0); texture = index
+ * into rt_scene_desc.textures (RT_TEXTURE only). */
+typedef struct {
+    int32_t kind; float color[3]; float color2[3]; float ior; float diffuse; int32_t texture;
+} rt_material;
+
+/* A Surface (template/template.cpp:1571-1601): 0x00RRGGBB texels, row-major.
+ * TextureMaterial indexes it as (u & (width-1)) + (v & (height-1)) * width. */
+typedef struct { const uint32_t *pixels; uint32_t width, height; } rt_texture;
 
 /* Scene description, the inputs of Scene::Scene (template/scene.h:40-128). */
 typedef struct {
@@ -79,6 +92,10 @@ typedef struct {
      * here with the reference's binned SAH (template/scene.h:845-976) */
     const void *bvh_nodes; uint32_t bvh_num_nodes; const uint32_t *bvh_indices;
     int32_t device;
+    /* per-primitive mat4 T (16 floats, row-major as rt_mat4_*), read for RT_CUBE and
+     * RT_QUAD only; NULL = identity for all (the factories' default argument) */
+    const float *transforms;
+    const rt_texture *textures; uint32_t num_textures;
 } rt_scene_desc;
 
 typedef struct { uint32_t num_prims, nodes_used, depth, max_leaf; } rt_scene_info;
@@ -128,8 +145,13 @@ int rt_mesh_to_prims(const float *verts, uint32_t nv, const int32_t *faces, uint
  * the counts, then with arrays of that size. */
 int rt_recipe_describe(const char *name, const char *mesh_dir, rt_prim *prims, uint32_t *num_prims,
                        rt_material *materials, uint32_t *num_materials);
-/* plain-BVH build only (no device): nodes (2N+2 x 32 B) and indices (N) */
-int rt_bvh_build_host(const rt_prim *prims, uint32_t n, void *nodes, uint32_t *indices, rt_scene_info *info);
+/* plain-BVH build only (no device): nodes (2N+2 x 32 B) and indices (N);
+ * transforms as in rt_scene_desc (NULL = identity) */
+int rt_bvh_build_host(const rt_prim *prims, const float *transforms, uint32_t n, void *nodes, uint32_t *indices,
+                      rt_scene_info *info);
+/* Surface::LoadImage (template/template.cpp:1579-1601) for PNG files (8/16-bit grey,
+ * grey+alpha, RGB, RGBA, palette; not interlaced): pixels = 0x00RRGGBB; free with rt_free. */
+int rt_image_load(const char *path, uint32_t **pixels, uint32_t *width, uint32_t *height);
 
 /* ---- scene (Scene, template/scene.h:37-1014) ------------------------------ */
 int rt_scene_create(const rt_scene_desc *desc, rt_scene **out);

@@ -60,6 +60,10 @@ def lib():
         L.or_scene_add_sphere.argtypes = [vp, fp, C.c_float, C.c_int]
         L.or_scene_add_plane.argtypes = [vp, fp, C.c_float, C.c_int]
         L.or_scene_add_triangle.argtypes = [vp, fp, fp, fp, C.c_int]
+        L.or_scene_add_material_tex.argtypes = [vp, C.c_int, fp, fp, C.c_float, C.c_float, C.c_int]
+        L.or_scene_add_texture.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_uint32)]
+        L.or_scene_add_cube.argtypes = [vp, fp, fp, fp, C.c_int]
+        L.or_scene_add_quad.argtypes = [vp, C.c_float, fp, C.c_int]
         L.or_scene_set_integrator.argtypes = [vp, C.c_int]
         L.or_scene_set_sky.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_uint32)]
         L.or_camera_default.argtypes = [C.POINTER(Camera), C.c_int, C.c_int]

@@ -173,13 +173,17 @@ typedef struct {
     int kind;         /* OR_* material kind */
     f3 c0, c1;        /* colour / absorption ; checkerboard colour2 */
     float ior, diffuse, specular;
+    int tex;          /* TextureMaterial: texture index */
 } material;
 
 typedef struct {
     int type, mat;
     f3 d[3];          /* Primitive::data (Primitive.h:25) */
     float M[16];      /* Primitive::Transform */
+    float Minv[16];   /* Primitive::InvertedTransform (FastInvertedTransformNoScale) */
 } prim;
+
+typedef struct { int w, h; uint32_t *px; } texture_t;
 
 typedef struct {      /* BVHNode.h:5-14 -- 32 bytes */
     float mn[3], mx[3];
@@ -192,6 +196,7 @@ struct or_scene {
     node *nodes; int nodesUsed, depth;
     uint32_t *idx;
     int skyW, skyH; uint32_t *sky;
+    texture_t *tex; int ntex;
     int integrator;   /* 0 = Renderer::Trace, 1 = Renderer::WhittedTrace (the K key, renderer.h:136-139) */
 };
 
@@ -217,6 +222,8 @@ or_scene *or_scene_new(void) {
 }
 void or_scene_free(or_scene *s) {
     if (!s) return;
+    for (int i = 0; i < s->ntex; i++) free(s->tex[i].px);
+    free(s->tex);
     free(s->p); free(s->m); free(s->nodes); free(s->idx); free(s->sky); free(s);
 }
 void or_scene_set_sky(or_scene *s, int w, int h, const uint32_t *px) {
@@ -224,7 +231,19 @@ void or_scene_set_sky(or_scene *s, int w, int h, const uint32_t *px) {
     s->sky = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)w * h);
     memcpy(s->sky, px, sizeof(uint32_t) * (size_t)w * h);
 }
+int or_scene_add_texture(or_scene *s, int w, int h, const uint32_t *px) {
+    s->tex = (texture_t *)realloc(s->tex, sizeof(texture_t) * (s->ntex + 1));
+    texture_t *t = &s->tex[s->ntex];
+    t->w = w; t->h = h;
+    t->px = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)w * h);
+    memcpy(t->px, px, sizeof(uint32_t) * (size_t)w * h);
+    return s->ntex++;
+}
 int or_scene_add_material(or_scene *s, int kind, const float c0[3], const float c1[3], float ior, float diffuse) {
+    return or_scene_add_material_tex(s, kind, c0, c1, ior, diffuse, -1);
+}
+int or_scene_add_material_tex(or_scene *s, int kind, const float c0[3], const float c1[3], float ior, float diffuse,
+                              int texture) {
     if (s->nm == s->capm) { s->capm = s->capm ? 2 * s->capm : 16; s->m = (material *)realloc(s->m, sizeof(material) * s->capm); }
     material *m = &s->m[s->nm];
     memset(m, 0, sizeof(*m));
@@ -232,9 +251,12 @@ int or_scene_add_material(or_scene *s, int kind, const float c0[3], const float 
     if (c0) m->c0 = mk(c0[0], c0[1], c0[2]);
     if (c1) m->c1 = mk(c1[0], c1[1], c1[2]);
     m->ior = ior;
-    /* Checkerboard.h:6-14: 2-arg ctor diffuse=1, specular=0; 3-arg clamps */
-    if (kind == OR_CHECKER) {
-        if (diffuse < 0.0f) { m->diffuse = 1.0f; m->specular = 0.0f; }
+    m->tex = texture;
+    /* Checkerboard.h:6-14 / TextureMaterial.h:6-17: short ctor diffuse=1, specular=0;
+     * with a diffuse argument clamp(diffuse, 0, 1) (precomp.h:782) and 1 - diffuse.
+     * DSMix.h:6-9 always takes the diffuse argument. */
+    if (kind == OR_CHECKER || kind == OR_TEXTURE || kind == OR_DSMIX) {
+        if (diffuse < 0.0f && kind != OR_DSMIX) { m->diffuse = 1.0f; m->specular = 0.0f; }
         else { m->diffuse = tmax_(0.0f, tmin_(diffuse, 1.0f)); m->specular = 1.0f - m->diffuse; }
     }
     return s->nm++;
@@ -244,6 +266,7 @@ static prim *push_prim(or_scene *s) {
     prim *p = &s->p[s->np++];
     memset(p, 0, sizeof(*p));
     memcpy(p->M, IDENT, 64);
+    memcpy(p->Minv, IDENT, 64);
     return p;
 }
 /* Primitive.h:690-698 */
@@ -252,6 +275,42 @@ int or_scene_add_sphere(or_scene *s, const float pos[3], float r, int mat) {
     p->type = OR_SPHERE; p->mat = mat;
     p->d[0] = mk(r, r * r, 1.0f / r);
     or_mat4_translate(p->M, pos[0], pos[1], pos[2]);
+    return s->np - 1;
+}
+/* mat4::FastInvertedTransformNoScale, template/precomp.h:1061-1085 (the non-SSE branch,
+ * same values): transpose of the 3x3 part, translation -(R^T t) */
+static void fast_inv(const float *c, float *r) {
+    memcpy(r, IDENT, 64);
+    r[0] = c[0], r[1] = c[4], r[2] = c[8];
+    r[4] = c[1], r[5] = c[5], r[6] = c[9];
+    r[8] = c[2], r[9] = c[6], r[10] = c[10];
+    r[3] = -(c[3] * r[0] + c[7] * r[1] + c[11] * r[2]);
+    r[7] = -(c[3] * r[4] + c[7] * r[5] + c[11] * r[6]);
+    r[11] = -(c[3] * r[8] + c[7] * r[9] + c[11] * r[10]);
+}
+/* Primitive.h:717-728 */
+int or_scene_add_cube(or_scene *s, const float pos[3], const float size[3], const float T[16], int mat) {
+    prim *p = push_prim(s);
+    p->type = OR_CUBE; p->mat = mat;
+    memcpy(p->M, T, 64);
+    f3 ps = mk(pos[0], pos[1], pos[2]);
+    if (length3(ps) > FLT_EPS_F) {
+        float Tr[16];
+        or_mat4_translate(Tr, pos[0], pos[1], pos[2]);
+        or_mat4_mul(p->M, T, Tr);
+    }
+    f3 sz = mk(size[0], size[1], size[2]);
+    p->d[0] = smul(-0.5f, sz); p->d[1] = smul(0.5f, sz);
+    fast_inv(p->M, p->Minv);
+    return s->np - 1;
+}
+/* Primitive.h:735-739 */
+int or_scene_add_quad(or_scene *s, float size, const float T[16], int mat) {
+    prim *p = push_prim(s);
+    p->type = OR_QUAD; p->mat = mat;
+    memcpy(p->M, T, 64);
+    p->d[0] = mk(0.5f * size, 0.0f, 0.0f);
+    fast_inv(p->M, p->Minv);
     return s->np - 1;
 }
 /* Primitive.h:705-710 */
@@ -290,21 +349,126 @@ static inline f3 prim_centroid(const prim *p) {   /* ctor 42-50, GetCentroid 443
     else if (p->type == OR_TRIANGLE) c = divs(add(add(p->d[0], p->d[1]), p->d[2]), 3.0f);
     return tpos(p->M, c);
 }
+/* the 8 cube corners / 4 quad corners in GetAABBMin/Max's order (Primitive.h:325-341) */
+static int box_corners(const prim *p, f3 *c) {
+    if (p->type == OR_CUBE) {
+        f3 a = p->d[0], b = p->d[1];
+        c[0] = tpos(p->M, a);
+        c[1] = tpos(p->M, mk(b.x, a.y, a.z));
+        c[2] = tpos(p->M, mk(a.x, b.y, a.z));
+        c[3] = tpos(p->M, mk(a.x, a.y, b.z));
+        c[4] = tpos(p->M, b);
+        c[5] = tpos(p->M, mk(a.x, b.y, b.z));
+        c[6] = tpos(p->M, mk(b.x, a.y, b.z));
+        c[7] = tpos(p->M, mk(b.x, b.y, a.z));
+        return 8;
+    }
+    float sz = p->d[0].x;   /* QUAD, Primitive.h:336-341 */
+    c[0] = tpos(p->M, mk(-sz, 0, -sz));
+    c[1] = tpos(p->M, mk(-sz, 0, sz));
+    c[2] = tpos(p->M, mk(sz, 0, -sz));
+    c[3] = tpos(p->M, mk(sz, 0, sz));
+    return 4;
+}
 static inline f3 prim_aabb_min(const prim *p) {   /* 319-351 */
     if (p->type == OR_SPHERE) return sub(tpos(p->M, mk(0, 0, 0)), mk(p->d[0].x, p->d[0].x, p->d[0].x));
     if (p->type == OR_PLANE) return mk(-1e30f, -1e30f, -1e30f);
+    if (p->type == OR_CUBE || p->type == OR_QUAD) {
+        f3 c[8];
+        int n = box_corners(p, c);
+        f3 m = c[0];
+        for (int i = 1; i < n; i++) m = fmin3(m, c[i]);
+        return m;
+    }
     f3 A = tpos(p->M, p->d[0]), B = tpos(p->M, p->d[1]), C = tpos(p->M, p->d[2]);
     return fmin3(A, fmin3(B, C));
 }
 static inline f3 prim_aabb_max(const prim *p) {   /* 356-388 */
     if (p->type == OR_SPHERE) return add(tpos(p->M, mk(0, 0, 0)), mk(p->d[0].x, p->d[0].x, p->d[0].x));
     if (p->type == OR_PLANE) return mk(1e30f, 1e30f, 1e30f);
+    if (p->type == OR_CUBE || p->type == OR_QUAD) {
+        f3 c[8];
+        int n = box_corners(p, c);
+        f3 m = c[0];
+        for (int i = 1; i < n; i++) m = fmax3(m, c[i]);
+        return m;
+    }
     f3 A = tpos(p->M, p->d[0]), B = tpos(p->M, p->d[1]), C = tpos(p->M, p->d[2]);
     return fmax3(A, fmax3(B, C));
 }
 
+/* CUBE slab test in object space (Primitive.h:87-110 / 196-235); returns 0 on a miss */
+static int cube_slab(const prim *p, const ray_t *r, float *tmin_o, float *tmax_o) {
+    f3 O = tpos(p->Minv, r->O), D = tvec(p->Minv, r->D);
+    float rDx = 1 / D.x, rDy = 1 / D.y, rDz = 1 / D.z;
+    int sx = D.x < 0, sy = D.y < 0, sz = D.z < 0;
+    const f3 *d = p->d;
+    float tmin = (d[sx].x - O.x) * rDx;
+    float tmax = (d[1 - sx].x - O.x) * rDx;
+    float tymin = (d[sy].y - O.y) * rDy;
+    float tymax = (d[1 - sy].y - O.y) * rDy;
+    if (tmin > tymax || tymin > tmax) return 0;
+    tmin = smax(tmin, tymin);
+    tmax = smin(tmax, tymax);
+    float tzmin = (d[sz].z - O.z) * rDz;
+    float tzmax = (d[1 - sz].z - O.z) * rDz;
+    if (tmin > tzmax || tzmin > tmax) return 0;
+    *tmin_o = smax(tmin, tzmin);
+    *tmax_o = smin(tmax, tzmax);
+    return 1;
+}
+/* Primitive::setTextureCoordsCube, Primitive.h:752-797 */
+static void cube_uv(const prim *p, ray_t *r) {
+    f3 objI = tpos(p->Minv, add(r->O, smul(r->t, r->D)));
+    const f3 *d = p->d;
+    float uc, vc;
+    float d0 = fabsf(objI.x - d[0].x), d1 = fabsf(objI.x - d[1].x);
+    float d2 = fabsf(objI.y - d[0].y), d3 = fabsf(objI.y - d[1].y);
+    float d4 = fabsf(objI.z - d[0].z), d5 = fabsf(objI.z - d[1].z);
+    float minDist = d0;
+    int face = 1;
+    uc = objI.z, vc = objI.y;
+    if (d1 < minDist) uc = -objI.z, vc = objI.y, face = 0, minDist = d1;
+    if (d2 < minDist) uc = objI.x, vc = objI.z, face = 3, minDist = d2;
+    if (d3 < minDist) uc = objI.x, vc = -objI.z, face = 2, minDist = d3;
+    if (d4 < minDist) uc = -objI.x, vc = objI.y, face = 5, minDist = d4;
+    if (d5 < minDist) uc = objI.x, vc = objI.y, face = 4;
+    uc = -uc, vc = -vc;
+    uc = 0.5f * (uc / d[1].x + 1.0f);
+    vc = 0.5f * (vc / d[1].x + 1.0f);
+    const float third = 1.0f / 3.0f;
+    switch (face) {
+    case 0: r->u = 0.25f * (2 + uc); r->v = third * (1 + vc); break;
+    case 1: r->u = 0.25f * (0 + uc); r->v = third * (1 + vc); break;
+    case 2: r->u = 0.25f * (1 + uc); r->v = third * vc; break;
+    case 3: r->u = 0.25f * (1 + uc); r->v = third * (2 + vc); break;
+    case 4: r->u = 0.25f * (1 + uc); r->v = third * (1 + vc); break;
+    default: r->u = 0.25f * (3 + uc); r->v = third * (1 + vc); break;
+    }
+}
+
 /* Primitive::Intersect, 149-279 */
 static void prim_intersect(const prim *p, ray_t *r, int idx) {
+    if (p->type == OR_CUBE) {   /* 195-235: note the acceptance test is on tmax */
+        float tmin, tmax;
+        if (!cube_slab(p, r, &tmin, &tmax)) return;
+        if (tmin > EPS_F) {
+            if (tmax < r->t) { r->t = tmin; r->obj = idx; cube_uv(p, r); }
+        } else if (tmax > EPS_F) {
+            if (tmax < r->t) { r->t = tmax; r->obj = idx; cube_uv(p, r); }
+        }
+        return;
+    }
+    if (p->type == OR_QUAD) {   /* 236-247; u, v are left unset there: defined as 0 here */
+        f3 O = tpos(p->Minv, r->O), D = tvec(p->Minv, r->D);
+        float t = O.y / -D.y;
+        float size = p->d[0].x;
+        if (t < r->t && t > EPS_F) {
+            f3 I = add(O, smul(t, D));
+            if (I.x > -size && I.x < size && I.z > -size && I.z < size) { r->t = t; r->obj = idx; r->u = r->v = 0.0f; }
+        }
+        return;
+    }
     if (p->type == OR_SPHERE) {
         f3 pos = tpos(p->M, mk(0, 0, 0));
         f3 oc = sub(r->O, pos);
@@ -330,6 +494,7 @@ static void prim_intersect(const prim *p, ray_t *r, int idx) {
             if (N.x < FLT_EPS_F && N.y < FLT_EPS_F) { r->u = I.x; r->v = -I.y; }
             else if (N.x < FLT_EPS_F && N.z < FLT_EPS_F) { r->u = I.x; r->v = -I.z; }
             else if (N.y < FLT_EPS_F && N.z < FLT_EPS_F) { r->u = I.y; r->v = -I.z; }
+            else { r->u = r->v = 0.0f; }   /* left unset by the reference: defined as 0 */
         }
     } else {
         f3 A = tpos(p->M, p->d[0]), B = tpos(p->M, p->d[1]), C = tpos(p->M, p->d[2]);
@@ -348,6 +513,16 @@ static void prim_intersect(const prim *p, ray_t *r, int idx) {
 
 /* Primitive::Hit, 64-144 */
 static int prim_hit(const prim *p, const ray_t *r) {
+    if (p->type == OR_CUBE) {   /* Primitive.h:83-110 */
+        float tmin, tmax;
+        if (!cube_slab(p, r, &tmin, &tmax)) return 0;
+        return (tmin > EPS_F || tmax > EPS_F) && tmax < r->t;
+    }
+    if (p->type == OR_QUAD) {   /* 111-117: the quad's extent is not tested (reference quirk) */
+        f3 O = tpos(p->Minv, r->O), D = tvec(p->Minv, r->D);
+        float t = O.y / -D.y;
+        return t < r->t && t > EPS_F;
+    }
     if (p->type == OR_SPHERE) {
         f3 pos = tpos(p->M, mk(0, 0, 0));
         f3 oc = sub(r->O, pos);
@@ -382,6 +557,22 @@ static int prim_hit(const prim *p, const ray_t *r) {
 static inline f3 prim_normal(const prim *p, f3 I) {
     if (p->type == OR_SPHERE) return muls(sub(I, tpos(p->M, mk(0, 0, 0))), p->d[0].z);
     if (p->type == OR_PLANE) return p->d[0];
+    if (p->type == OR_CUBE) {   /* Primitive.h:290-305 */
+        f3 objI = tpos(p->Minv, I);
+        const f3 *d = p->d;
+        f3 N = mk(-1, 0, 0);
+        float d0 = fabsf(objI.x - d[0].x), d1 = fabsf(objI.x - d[1].x);
+        float d2 = fabsf(objI.y - d[0].y), d3 = fabsf(objI.y - d[1].y);
+        float d4 = fabsf(objI.z - d[0].z), d5 = fabsf(objI.z - d[1].z);
+        float minDist = d0;
+        if (d1 < minDist) minDist = d1, N.x = 1;
+        if (d2 < minDist) minDist = d2, N = mk(0, -1, 0);
+        if (d3 < minDist) minDist = d3, N = mk(0, 1, 0);
+        if (d4 < minDist) minDist = d4, N = mk(0, 0, -1);
+        if (d5 < minDist) minDist = d5, N = mk(0, 0, 1);
+        return tvec(p->M, N);
+    }
+    if (p->type == OR_QUAD) return tvec(p->M, mk(0, -1, 0));   /* 306-307 */
     f3 baseN = normalize(cross(sub(p->d[2], p->d[0]), sub(p->d[1], p->d[0])));
     return tvec(p->M, baseN);
 }
@@ -601,12 +792,36 @@ static f3 sphere_random_point(const prim *p, uint32_t *seed) {
 static inline float prim_area(const prim *p) {   /* 450-468 */
     if (p->type == OR_SPHERE) return 4.0f * PI_F * p->d[0].y;
     if (p->type == OR_PLANE) return 1e30f;
+    if (p->type == OR_CUBE) {
+        f3 sz = smul(2.0f, p->d[1]);
+        return 2.0f * (sz.x * sz.y + sz.x * sz.z + sz.y * sz.z);
+    }
+    if (p->type == OR_QUAD) { float sz = 2.0f * p->d[0].x; return sz * sz; }
     f3 AB = sub(p->d[1], p->d[0]), AC = sub(p->d[2], p->d[0]);
     return 0.5f * length3(cross(AB, AC));
 }
 static f3 light_random_point(const prim *p, uint32_t *seed) {
     if (p->type == OR_SPHERE) return sphere_random_point(p, seed);
     if (p->type == OR_PLANE) return muls(neg(p->d[0]), p->d[1].x);
+    if (p->type == OR_CUBE) {   /* Primitive.h:405-422 (Rand(6) = RandomFloat() * 6) */
+        float u = rnd_f(seed) * 2.0f - 1.0f;
+        float v = rnd_f(seed) * 2.0f - 1.0f;
+        float face = rnd_f(seed) * 6.0f;
+        f3 q;
+        if (face < 1) q = mk(-1, u, v);
+        else if (face < 2) q = mk(1, u, v);
+        else if (face < 3) q = mk(u, -1, v);
+        else if (face < 4) q = mk(u, 1, v);
+        else if (face < 5) q = mk(u, v, -1);
+        else q = mk(u, v, 1);
+        return tpos(p->M, mul(q, p->d[1]));
+    }
+    if (p->type == OR_QUAD) {   /* 423-427: the point lies in object z = 0 (reference quirk) */
+        float size = p->d[0].x;
+        float a = size * (rnd_f(seed) - 1.0f);
+        float b = size * (rnd_f(seed) - 1.0f);
+        return tpos(p->M, mk(a, b, 0.0f));
+    }
     float u = rnd_f(seed), v = rnd_f(seed);   /* Primitive.h:429-437 */
     while ((u + v) > 1) { u = rnd_f(seed); v = rnd_f(seed); }
     return tpos(p->M, add(add(p->d[0], smul(u, p->d[1])), smul(v, p->d[2])));
@@ -735,8 +950,19 @@ static int mat_scatter(const material *m, const ray_t *in, f3 I, f3 N, ray_t *ou
         return 0;
     }
 }
-static f3 mat_color(const material *m, const ray_t *in) {
+/* TextureMaterial::GetColor, TextureMaterial.h:30-37 */
+static f3 texture_color(const or_scene *s, const material *m, const ray_t *in, float scale) {
+    const texture_t *t = &s->tex[m->tex];
+    uint32_t u = f2u_wrap((float)t->w * in->u);
+    uint32_t v = f2u_wrap((float)t->h * in->v);
+    uint32_t idx = (u & (uint32_t)(t->w - 1)) + (v & (uint32_t)(t->h - 1)) * (uint32_t)t->w;
+    uint32_t p = t->px[idx];
+    return muls(mk((float)((p >> 16) & 255), (float)((p >> 8) & 255), (float)(p & 255)), scale);
+}
+static f3 mat_color(const or_scene *s, const material *m, const ray_t *in) {
     switch (m->kind) {
+    case OR_TEXTURE:
+        return texture_color(s, m, in, 1.0f / 255.0f);   /* TextureMaterial::correction */
     case OR_DIELECTRIC: {   /* Dielectric.h:12-21 */
         f3 c = mk(1, 1, 1);
         if (in->inside) {
@@ -775,7 +1001,7 @@ static f3 nee(const or_scene *s, f3 I, f3 N, f3 BRDF, uint32_t *seed, counters *
         if (!is_occluded(s, &sh, k)) {
             float solid = (dotNlL * area) / (dist * dist);
             float lightPDF = 1.0f / solid;
-            Ld = muls(mul(mat_color(&s->m[lp->mat], &sh), BRDF), (dotNL / lightPDF));
+            Ld = muls(mul(mat_color(s, &s->m[lp->mat], &sh), BRDF), (dotNL / lightPDF));
         }
     }
     return Ld;
@@ -791,7 +1017,7 @@ static f3 trace(const or_scene *s, ray_t *ray, int lastSpecular, int depth, uint
     const material *m = &s->m[s->p[ray->obj].mat];
     ray_t out = mkray(mk(0, 0, 0), mk(1, 1, 1), 1e34f);
     int spec = mat_scatter(m, ray, I, N, &out, seed);
-    f3 albedo = mat_color(m, ray);
+    f3 albedo = mat_color(s, m, ray);
     int flag = mat_flag(m);
     if (flag == FLAG_DIFFUSE || (flag == FLAG_MIX && !spec)) {
         f3 BRDF = muls(albedo, INVPI_F);
@@ -809,16 +1035,24 @@ static f3 trace(const or_scene *s, ray_t *ray, int lastSpecular, int depth, uint
 
 /* ObjectMaterial::getColorModifier overrides (Whitted colour + parameters):
  * Diffuse.h:21-23, Mirror.h:21-23, Light.h:20-22, Checkerboard.h:60-71, Dielectric.h:56-85 */
-static void color_modifier(const material *m, const ray_t *in, f3 N, float cv[7]) {
+static void color_modifier(const or_scene *s, const material *m, const ray_t *in, f3 N, float cv[7]) {
     memset(cv, 0, 7 * sizeof(float));
     switch (m->kind) {
     case OR_LIGHT:
         /* template/precomp.h:782 clamp = fmaxf(a, fminf(f, b)) */
-        cv[0] = fmaxf(0.0f, fminf(m->c0.x, 1.0f)); cv[1] = fmaxf(0.0f, fminf(m->c0.y, 1.0f));
-        cv[2] = fmaxf(0.0f, fminf(m->c0.z, 1.0f));
+        cv[0] = tmax_(0.0f, tmin_(m->c0.x, 1.0f)); cv[1] = tmax_(0.0f, tmin_(m->c0.y, 1.0f));
+        cv[2] = tmax_(0.0f, tmin_(m->c0.z, 1.0f));
         return;
     case OR_CHECKER: {
-        f3 c = mat_color(m, in);
+        f3 c = mat_color(s, m, in);
+        cv[0] = c.x; cv[1] = c.y; cv[2] = c.z; cv[3] = m->diffuse;
+        return;
+    }
+    case OR_DSMIX:   /* DSMix.h:48-50 */
+        cv[0] = m->c0.x; cv[1] = m->c0.y; cv[2] = m->c0.z; cv[3] = m->diffuse;
+        return;
+    case OR_TEXTURE: {   /* TextureMaterial.h:62-71 (SKYDOME_CORRECTION) */
+        f3 c = texture_color(s, m, in, SKYDOME_CORRECTION_F);
         cv[0] = c.x; cv[1] = c.y; cv[2] = c.z; cv[3] = m->diffuse;
         return;
     }
@@ -880,7 +1114,7 @@ static f3 whitted(const or_scene *s, ray_t *ray, int depth, uint32_t *seed, coun
     const material *m = &s->m[s->p[ray->obj].mat];
     int flag = mat_flag(m);
     float cv[7];
-    color_modifier(m, ray, N, cv);
+    color_modifier(s, m, ray, N, cv);
     if (flag == FLAG_LIGHT) {
         result = add(result, mk(24, 24, 22));
     } else if (flag == FLAG_DIFFUSE) {
@@ -976,7 +1210,7 @@ static f3 shade_packet_ray(const or_scene *s, ray_t *ray, int depth, uint32_t *s
     const material *m = &s->m[s->p[ray->obj].mat];
     ray_t out = mkray(mk(0, 0, 0), mk(1, 1, 1), 1e34f);
     int spec = mat_scatter(m, ray, I, N, &out, seed);
-    f3 albedo = mat_color(m, ray);
+    f3 albedo = mat_color(s, m, ray);
     int flag = mat_flag(m);
     if (flag == FLAG_DIFFUSE || flag == FLAG_MIX) {
         /* MIX: a specular bounce is traced once for a result that is then overwritten

@@ -26,9 +26,9 @@ extern "C" {
 #endif
 
 /* material kinds (MaterialType.h:3-9 + the concrete classes) */
-enum { OR_DIFFUSE = 0, OR_MIRROR = 1, OR_DIELECTRIC = 2, OR_CHECKER = 3, OR_LIGHT = 4 };
+enum { OR_DIFFUSE = 0, OR_MIRROR = 1, OR_DIELECTRIC = 2, OR_CHECKER = 3, OR_LIGHT = 4, OR_DSMIX = 5, OR_TEXTURE = 6 };
 /* primitive kinds (Primitive.h:8-14) */
-enum { OR_SPHERE = 0, OR_PLANE = 1, OR_TRIANGLE = 4 };
+enum { OR_SPHERE = 0, OR_PLANE = 1, OR_CUBE = 2, OR_QUAD = 3, OR_TRIANGLE = 4 };
 /* probe modes (SURVEY.md Appendix A / BASELINE.md section 2) */
 enum { OR_PROBE_PRIMARY = 0, OR_PROBE_PS = 1, OR_PROBE_PT = 2 };
 
@@ -70,6 +70,15 @@ void or_mat4_mul(float r[16], const float a[16], const float b[16]);
 or_scene *or_scene_new(void);
 void or_scene_free(or_scene *s);
 int or_scene_add_material(or_scene *s, int kind, const float c0[3], const float c1[3], float ior, float diffuse);
+/* TextureMaterial (TextureMaterial.h:6-17): texture = index from or_scene_add_texture */
+int or_scene_add_material_tex(or_scene *s, int kind, const float c0[3], const float c1[3], float ior, float diffuse,
+                              int texture);
+/* Surface pixels 0x00RRGGBB (template/template.cpp:1579-1601), w x h */
+int or_scene_add_texture(or_scene *s, int w, int h, const uint32_t *pixels);
+/* Primitive::createCube (Primitive.h:717-728): T * Translate(pos) when |pos| > FLT_EPSILON */
+int or_scene_add_cube(or_scene *s, const float pos[3], const float size[3], const float T[16], int mat);
+/* Primitive::createQuad (Primitive.h:735-739) */
+int or_scene_add_quad(or_scene *s, float size, const float T[16], int mat);
 int or_scene_add_sphere(or_scene *s, const float pos[3], float r, int mat);
 int or_scene_add_plane(or_scene *s, const float n[3], float d, int mat);
 int or_scene_add_triangle(or_scene *s, const float v0[3], const float v1[3], const float v2[3], int mat);

@@ -184,25 +184,33 @@ def test_sharded_frame_assembles_to_full_frame(rt, scenes, torch):
     assert np.array_equal(host, full.cpu().numpy())
 
 
-def twin_scene(rt, oracle, prims, mats, sky=None):
+def twin_scene(rt, oracle, prims, mats, sky=None, textures=()):
     """The same hand-made scene in the product (device) and in the oracle."""
-    o = oracle_scene(rt, oracle, prims, mats, sky)
-    return rt.Scene(prims, mats, sky=sky), o
+    o = oracle_scene(rt, oracle, prims, mats, sky, textures)
+    return rt.Scene(prims, mats, sky=sky, textures=textures), o
 
 
-def oracle_scene(rt, oracle, prims, mats, sky=None):
+def oracle_scene(rt, oracle, prims, mats, sky=None, textures=()):
     import ctypes as C
     L = oracle.lib()
     h = L.or_scene_new()
     f3 = lambda *v: (C.c_float * 3)(*v)
+    f16 = lambda T: (C.c_float * 16)(*(np.eye(4, dtype=np.float32).reshape(16) if T is None else T))
+    for t in textures:
+        t = np.ascontiguousarray(t, np.uint32)
+        L.or_scene_add_texture(h, t.shape[1], t.shape[0], t.ctypes.data_as(C.POINTER(C.c_uint32)))
     for m in mats:
-        L.or_scene_add_material(h, m.kind, f3(*m.color), f3(*m.color2), m.ior, m.diffuse)
+        L.or_scene_add_material_tex(h, m.kind, f3(*m.color), f3(*m.color2), m.ior, m.diffuse, m.texture)
     for p in prims:
         v = list(p.v)
         if p.type == rt.SPHERE:
             L.or_scene_add_sphere(h, f3(*v[:3]), v[3], p.material)
         elif p.type == rt.PLANE:
             L.or_scene_add_plane(h, f3(*v[:3]), v[3], p.material)
+        elif p.type == rt.CUBE:
+            L.or_scene_add_cube(h, f3(*v[:3]), f3(*v[3:6]), f16(getattr(p, "T", None)), p.material)
+        elif p.type == rt.QUAD:
+            L.or_scene_add_quad(h, v[0], f16(getattr(p, "T", None)), p.material)
         else:
             L.or_scene_add_triangle(h, f3(*v[:3]), f3(*v[3:6]), f3(*v[6:9]), p.material)
     if sky is not None:
@@ -381,4 +389,59 @@ def test_wave_camera_walk_bit_exact(rt, oracle, torch, name, W, H):
     got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, W, H, 1, 1, frames=2)
     assert np.array_equal(got, want)
     assert np.array_equal(gacc.view(np.uint32), acc.view(np.uint32))
+    assert c["shadow"] == st["shadow"]
+
+
+# ---- cubes, quads, DSMix, TextureMaterial (Primitive.h:195-247, DSMix.h, TextureMaterial.h)
+def shapes_scene(rt, oracle, make=twin_scene, quad_light=False):
+    rng = np.random.default_rng(11)
+    tex = [rng.integers(0, 1 << 24, size=(64, 128), dtype=np.uint32),
+           rng.integers(0, 1 << 24, size=(32, 32), dtype=np.uint32)]
+    mats = [rt.material(rt.LIGHT, (24, 24, 22)), rt.material(rt.DSMIX, (0.8, 0.6, 0.2), diffuse=0.4),
+            rt.material(rt.TEXTURE, texture=0), rt.material(rt.TEXTURE, texture=1, diffuse=0.7),
+            rt.material(rt.DSMIX, (0.3, 0.9, 0.9), diffuse=0.0), rt.material(rt.DIFFUSE, (0.7, 0.7, 0.7)),
+            rt.material(rt.DIELECTRIC, (0.1, 0.3, 0.1), ior=1.4), rt.material(rt.CHECKERBOARD, (0.1, 0.1, 0.1), (0.9, 0.9, 0.9))]
+    R = rt.mat4_mul(rt.mat4_translate(0.9, -0.2, 2.6), rt.mat4_rotate(1, 0.6), rt.mat4_rotate(0, 0.3))
+    light = (rt.quad(1.5, 0, rt.mat4_translate(0.0, 2.5, 1.5)) if quad_light else rt.sphere((0, 4, -2), 0.5, 0))
+    prims = [light,
+             rt.cube((0, 0, 0), (0.8, 0.6, 0.7), 2, R),                      # textured, rotated cube
+             rt.cube((-1.0, -0.3, 2.2), (0.5, 0.5, 0.5), 1),                 # DSMix cube, pos != 0
+             rt.cube((0.2, 0.9, 3.0), 0.6, 6),                               # glass cube
+             rt.quad(4.0, 7, rt.mat4_translate(0, -1.0, 2.0)),               # checkerboard floor quad
+             rt.quad(1.2, 4, rt.mat4_mul(rt.mat4_translate(-1.2, 0.6, 3.5), rt.mat4_rotate(0, -1.2))),
+             rt.sphere((1.2, 0.8, 2.0), 0.45, 3),                            # textured sphere (atan2 uv)
+             rt.plane((0, 0, -1), 6.0, 5),
+             rt.triangle((-2, -1, 4), (2, -1, 4), (0, 2, 4.5), 2)]           # textured triangle (barycentric uv)
+    return make(rt, oracle, prims, mats, textures=tex)
+
+
+def test_shapes_hits_bit_exact(rt, oracle, torch):
+    g, o = shapes_scene(rt, oracle)
+    W, H = 320, 200
+    rays = o.camera_rays(W, H, np.arange(W * H, dtype=np.int32))
+    hits_equal(g.IntersectBVH(rays), o.intersect(rays))
+    rays = random_rays(30000, 21)
+    hits_equal(g.IntersectBVH(rays), o.intersect(rays))
+    occl = rays.copy()
+    occl[:, 6] = 2.0
+    assert np.array_equal(g.IsOccluded(occl).cpu().numpy(), o.occluded(occl).astype(bool))
+    hits_equal(g.IntersectBVHPacket(rays), o.intersect_packets(rays))
+    with pytest.raises(rt.RTError):
+        g.set_camera_walk(rt.WALK_WAVE)   # cubes: acceptance depends on the visiting order
+
+
+@pytest.mark.parametrize("mode,depth,spp", [(0, 1, 1), (0, 6, 2), (1, 20, 1), (2, 5, 1)])
+def test_shapes_frames(rt, oracle, torch, mode, depth, spp):
+    g, o = shapes_scene(rt, oracle)
+    got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, 160, 100, spp, depth, mode=mode)
+    assert np.abs(gacc - acc).max() <= PIX_TOL
+    assert np.array_equal(got, want), f"{(got != want).sum()} RGB8 mismatches"
+    assert c["shadow"] == st["shadow"]
+
+
+@pytest.mark.parametrize("mode,depth", [(0, 4), (1, 10)])
+def test_quad_light(rt, oracle, torch, mode, depth):
+    g, o = shapes_scene(rt, oracle, quad_light=True)
+    got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, 120, 80, 1, depth, mode=mode)
+    assert np.abs(gacc - acc).max() <= PIX_TOL
     assert c["shadow"] == st["shadow"]

@@ -56,7 +56,7 @@ def test_compat_header_compiles(rt, tmp_path):
 
 
 def test_abi_version_and_device_count(rt):
-    assert rt.lib().rt_abi_version() == 1
+    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 2
     assert rt.device_count() >= 0
 
 

@@ -8,13 +8,17 @@
 //     stack and precomputed per-primitive bounds, producing the identical node array;
 //   * the SURVEY.md 8(d) benchmark scenes.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iterator>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <zlib.h>
@@ -260,6 +264,11 @@ inline float area(const Box &b) {                                               
     return smax(0.0f, e0 * e1 + e0 * e2 + e1 * e2);
 }
 
+// The reference's recursive Subdivide (template/scene.h:866-910) on a thread pool: a node's
+// split only reads and reorders its own index range, so subtrees are independent; child
+// pairs are allocated in whatever order the workers finish and renumbered afterwards in
+// the recursion's pre-order (left subtree before right), which reproduces nodesUsed's
+// allocation order.  Nodes, indices, depth: identical to the sequential build.
 class Builder {
   public:
     Builder(const std::vector<PrimGeom> &g, Bvh &b) : geo_(g), bvh_(b) {}
@@ -267,19 +276,21 @@ class Builder {
     void run(uint32_t n) {
         bvh_.indices.resize(n);
         for (uint32_t i = 0; i < n; ++i) bvh_.indices[i] = i;
-        bvh_.nodes.assign(2 * (size_t)n + 2, Node{});
-        bvh_.nodes[0].leftFirst = 0;
-        bvh_.nodes[0].count = n;
-        bvh_.nodes_used = 2;   // node 1 skipped for 64-byte child pairs (scene.h:849)
+        tmp_.assign(2 * (size_t)n + 2, Node{});
+        kid_.assign(2 * (size_t)n + 2, 0u);
+        tmp_[0].leftFirst = 0;
+        tmp_[0].count = n;
+        used_ = 2;   // node 1 skipped for 64-byte child pairs (scene.h:849)
         refit(0);
-        // depth-first, left before right: the same allocation order as the recursion
-        std::vector<uint32_t> work{0};
-        while (!work.empty()) {
-            uint32_t ni = work.back();
-            work.pop_back();
-            uint32_t l;
-            if (split(ni, l)) { work.push_back(l + 1); work.push_back(l); }
-        }
+        unsigned hw = std::thread::hardware_concurrency();
+        unsigned nt = n < 4 * kTaskMin ? 1u : std::max(1u, std::min(16u, hw ? hw : 1u));
+        queue_.push_back(0);
+        pending_ = 1;
+        std::vector<std::thread> pool;
+        for (unsigned t = 1; t < nt; ++t) pool.emplace_back([this] { worker(); });
+        worker();
+        for (auto &t : pool) t.join();
+        renumber();
         bvh_.depth = depth(0);
         bvh_.max_leaf = 0;
         for (uint32_t i = 0; i < bvh_.nodes_used; ++i)
@@ -287,11 +298,71 @@ class Builder {
     }
 
   private:
+    static constexpr uint32_t kTaskMin = 2048;   // smaller subtrees stay with their worker
     const std::vector<PrimGeom> &geo_;
     Bvh &bvh_;
+    std::vector<Node> tmp_;            // nodes in allocation order
+    std::vector<uint32_t> kid_;        // tmp index of an interior node's left child
+    std::atomic<uint32_t> used_{2};
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<uint32_t> queue_;      // subtrees waiting for a worker
+    uint32_t pending_ = 0;             // queued + running subtrees
+
+    void worker() {
+        for (;;) {
+            uint32_t root;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return !queue_.empty() || pending_ == 0; });
+                if (queue_.empty()) return;
+                root = queue_.back();
+                queue_.pop_back();
+            }
+            std::vector<uint32_t> work{root};
+            while (!work.empty()) {
+                const uint32_t ni = work.back();
+                work.pop_back();
+                uint32_t l;
+                if (!split(ni, l)) continue;
+                for (uint32_t c : {l + 1, l}) {
+                    if (tmp_[c].count >= kTaskMin) {
+                        std::lock_guard<std::mutex> lk(mu_);
+                        queue_.push_back(c);
+                        ++pending_;
+                        cv_.notify_one();
+                    } else {
+                        work.push_back(c);
+                    }
+                }
+            }
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) cv_.notify_all();
+        }
+    }
+
+    // final ids: pairs handed out in the recursion's pre-order
+    void renumber() {
+        bvh_.nodes.assign(tmp_.size(), Node{});
+        bvh_.nodes_used = 2;
+        std::vector<std::pair<uint32_t, uint32_t>> st{{0u, 0u}};   // (tmp id, final id)
+        while (!st.empty()) {
+            auto [t, f] = st.back();
+            st.pop_back();
+            Node nd = tmp_[t];
+            if (nd.count == 0) {
+                const uint32_t pair = bvh_.nodes_used;
+                bvh_.nodes_used += 2;
+                nd.leftFirst = pair;
+                st.push_back({kid_[t] + 1, pair + 1});
+                st.push_back({kid_[t], pair});
+            }
+            bvh_.nodes[f] = nd;
+        }
+    }
 
     void refit(uint32_t ni) {   // UpdateNodeBounds
-        Node &n = bvh_.nodes[ni];
+        Node &n = tmp_[ni];
         f3 mn = mk(1e30f, 1e30f, 1e30f), mx = mk(-1e30f, -1e30f, -1e30f);
         for (uint32_t i = 0; i < n.count; ++i) {
             const PrimGeom &g = geo_[bvh_.indices[n.leftFirst + i]];
@@ -343,7 +414,7 @@ class Builder {
     }
 
     bool split(uint32_t ni, uint32_t &left) {   // Subdivide, minus the recursion
-        Node n = bvh_.nodes[ni];
+        Node n = tmp_[ni];
         int axis = 0;
         float pos = 0.0f;
         float cost = best_plane(n, axis, pos);
@@ -357,13 +428,13 @@ class Builder {
         }
         int lcount = i - (int)n.leftFirst;
         if (lcount == 0 || lcount == (int)n.count) return false;
-        left = bvh_.nodes_used;
-        bvh_.nodes_used += 2;
-        Node &l = bvh_.nodes[left], &r = bvh_.nodes[left + 1];
+        left = used_.fetch_add(2);
+        Node &l = tmp_[left], &r = tmp_[left + 1];
         l.leftFirst = n.leftFirst; l.count = (uint32_t)lcount;
         r.leftFirst = (uint32_t)i; r.count = n.count - (uint32_t)lcount;
-        bvh_.nodes[ni].leftFirst = left;
-        bvh_.nodes[ni].count = 0;
+        kid_[ni] = left;
+        tmp_[ni].leftFirst = left;
+        tmp_[ni].count = 0;
         refit(left);
         refit(left + 1);
         return true;

@@ -148,6 +148,45 @@ def test_bvh_identical_to_oracle(rt, oracle, name):
     assert np.array_equal(idx, o.indices())
 
 
+def test_parallel_bvh_build_matches_oracle_on_soups(rt, oracle):
+    """The thread-pool builder renumbers to the recursion's order: identical trees on
+    large random soups (clustered + uniform), with cubes / quads / spheres mixed in."""
+    import ctypes as C
+    rng = np.random.default_rng(3)
+    n = 60000
+    centers = np.concatenate([rng.normal(0, 0.3, (n // 2, 3)), rng.uniform(-5, 5, (n - n // 2, 3))]).astype(np.float32)
+    V = (centers[:, None, :] + rng.normal(0, 0.02, (n, 3, 3))).astype(np.float32)
+    prims = [rt.sphere((0, 4, -2), 0.5, 0)] + [rt.triangle(*map(tuple, V[i]), 0) for i in range(n)]
+    prims += [rt.cube((0.5, 0, 0), (0.3, 0.2, 0.4), 0, rt.mat4_rotate(1, 0.4)), rt.quad(0.7, 0, rt.mat4_translate(1, 1, 1)),
+              rt.sphere((1, 2, 3), 0.25, 0)]
+    nodes, idx, info = rt.build_bvh_host(prims)
+    L = oracle.lib()
+    h = L.or_scene_new()
+    f3 = lambda *v: (C.c_float * 3)(*v)
+    f16 = lambda T: (C.c_float * 16)(*(np.eye(4, dtype=np.float32).reshape(16) if T is None else T))
+    L.or_scene_add_material(h, 0, f3(1, 1, 1), f3(0, 0, 0), 0.0, -1.0)
+    for p in prims:
+        v = list(p.v)
+        if p.type == rt.SPHERE:
+            L.or_scene_add_sphere(h, f3(*v[:3]), v[3], 0)
+        elif p.type == rt.CUBE:
+            L.or_scene_add_cube(h, f3(*v[:3]), f3(*v[3:6]), f16(p.T), 0)
+        elif p.type == rt.QUAD:
+            L.or_scene_add_quad(h, v[0], f16(p.T), 0)
+        else:
+            L.or_scene_add_triangle(h, f3(*v[:3]), f3(*v[3:6]), f3(*v[6:9]), 0)
+    L.or_scene_build_bvh(h)
+    o = oracle.Scene.__new__(oracle.Scene)
+    o.L, o.h = L, h
+    on = o.nodes().copy()
+    nodes = nodes.copy()
+    on[1] = 0
+    nodes[1] = 0
+    assert info["nodes_used"] == o.nodes_used and info["depth"] == o.depth
+    assert np.array_equal(nodes, on)
+    assert np.array_equal(idx, o.indices())
+
+
 def test_bvh_small_and_degenerate_inputs(rt):
     light = rt.sphere((0, 4, -2), 0.5, 0)
     # a single primitive: the root is a leaf (maxDepthBVH returns 1)

@@ -12,8 +12,10 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librtamd.so")
-SOURCES = ["rt_host.cpp", "rt_device.hip"]
-HEADERS = ["rt_math.h", "rt_internal.h", "rt_libm.h", os.path.join("..", "..", "include", "rt_amd.h")]
+# the kernels are compiled twice (core / extension builds of rt_kernels.inc), in parallel
+SOURCES = ["rt_host.cpp", "rt_device.hip", "rt_kern_core.hip", "rt_kern_ext.hip"]
+HEADERS = ["rt_math.h", "rt_internal.h", "rt_libm.h", "rt_dev_types.h", "rt_kernels.inc",
+           os.path.join("..", "..", "include", "rt_amd.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off + IEEE div/sqrt (hipcc's default) keep the kernels' float results
@@ -34,12 +36,29 @@ def _stale():
 def build(force=False, verbose=False):
     if not force and not _stale():
         return LIB
-    cmd = [HIPCC] + FLAGS + ["-o", LIB + ".tmp"] + [os.path.join(CSRC, f) for f in SOURCES] + LIBS
+    objdir = os.path.join(PKG, "_obj")
+    os.makedirs(objdir, exist_ok=True)
+    compile_flags = [f for f in FLAGS if f != "-shared"]
+    procs = []
+    objs = []
+    for f in SOURCES:   # one hipcc per translation unit, concurrently
+        obj = os.path.join(objdir, os.path.splitext(f)[0] + ".o")
+        lang = ["-x", "hip"]
+        cmd = [HIPCC] + compile_flags + lang + ["-c", os.path.join(CSRC, f), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((f, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
+        objs.append(obj)
+    for f, p in procs:
+        out, err = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {f} ({p.returncode}):\n{out}\n{err}")
+    cmd = [HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared", "--hip-link", "-o", LIB + ".tmp"] + objs + LIBS
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
+        raise RuntimeError(f"link failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
     os.replace(LIB + ".tmp", LIB)
     return LIB
 

@@ -1,0 +1,91 @@
+// rt_dev_types.h -- the device scene / frame records shared by the host code
+// (rt_device.hip) and the two kernel builds (rt_kern_core.hip, rt_kern_ext.hip), and the
+// launchers each kernel build exports.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/rt_amd.h"
+
+namespace rt {
+
+enum : uint32_t { T_TRI = 4, T_SPH = 0, T_PLANE = 1, T_CUBE = 2, T_QUAD = 3 };
+enum : int { F_DIFFUSE = 0, F_SPECULAR = 1, F_MIX = 2, F_DIELECTRIC = 3, F_LIGHT = 4 };
+
+struct DevMaterial {
+    int kind, flag;
+    float c0[3], c1[3];
+    float ior, diffuse, specular;
+    uint32_t tex_off, tex_w, tex_h;   // TextureMaterial: texels at SceneView::tex + tex_off
+};
+
+struct SceneView {
+    const float4 *__restrict__ nodes;   // 2 float4 per node
+    const float4 *__restrict__ pairs;   // 4 float4 per child pair (X, Y, Z, words), pair k at 4k
+    const float4 *__restrict__ prims;   // 3 float4 per leaf slot
+    const float4 *__restrict__ shade;   // 2 float4 per primitive id
+    const DevMaterial *__restrict__ mats;
+    const uint32_t *__restrict__ sky;
+    const float4 *__restrict__ xprims;  // cubes / quads: 8 float4 each (Minv rows, M rows, data)
+    const uint32_t *__restrict__ tex;   // all TextureMaterial texels
+    uint32_t sky_w, sky_h;
+    int sky_const;
+    float sky_rgb[3];
+    float light_M[12];                  // prim 0 Transform rows 0..2
+    float light_c[3];
+    float light_r, light_r2, light_invr;
+    int light_mat;
+    int light_quad;                     // prim 0 is a quad (else a sphere)
+    float light_qsize, light_area;      // quad data[0].x; Primitive::GetArea
+    float light_N[3];                   // quad normal TransformVector((0,-1,0), M)
+    uint32_t root_word;
+    int bounds_finite;                  // every node bound is a finite float
+    uint32_t stack_entries;             // LDS stack entries per lane
+    uint32_t node_f4;                   // node array size in float4s
+    int wave_primary;                   // camera rays take the wave-coherent walk
+};
+
+struct FrameArgs {
+    float cam_pos[3], cam_tl[3], cam_tr[3], cam_bl[3];
+    float lens, rw, rh;
+    uint32_t W, H, spp, depth, frame, reset;
+    uint32_t shard, nshards, tiles_x, ntiles_local;
+    int packed_out;
+    float4 *acc;
+    uint32_t *out;
+    unsigned long long *counters;       // [0] shadow rays, [1] bounce rays
+};
+
+// One launch of the frame kernel family (Renderer::Tick): integrator mode, Trace depth
+// bucket, textured sky, LDS-node kernel.
+struct FrameLaunch {
+    int mode;        // RT_MODE_*
+    int md;          // depth bucket: 1, 4, 10 or 32
+    bool tex;        // non-constant sky texture
+    bool lds;        // k_render_lds (primary+shadow, nodes in LDS)
+    dim3 grid, block;
+    size_t lds_bytes;
+    hipStream_t stream;
+};
+
+// Each kernel build provides the same launchers: `kcore` is compiled without the
+// extension primitives and materials (cubes, quads, quad light, TextureMaterial,
+// non-Light light materials), `kext` with them.  The host picks per scene.
+#define RT_DECLARE_LAUNCHERS(NS)                                                                  \
+    namespace NS {                                                                                \
+    void launch_frame(const SceneView &S, const FrameArgs &F, const FrameLaunch &L);              \
+    void launch_intersect(const SceneView &S, const rt_ray *rays, rt_hit *hits, uint32_t n,       \
+                          size_t lds, hipStream_t st);                                            \
+    void launch_occluded(const SceneView &S, const rt_ray *rays, uint8_t *out, uint32_t n,        \
+                         size_t lds, hipStream_t st);                                             \
+    void launch_intersect_packet(const SceneView &S, const rt_ray *rays, rt_hit *hits,            \
+                                 uint32_t n, hipStream_t st);                                     \
+    }
+RT_DECLARE_LAUNCHERS(kcore)
+RT_DECLARE_LAUNCHERS(kext)
+#undef RT_DECLARE_LAUNCHERS
+void launch_assemble(const uint32_t *gathered, uint32_t cap, uint32_t nshards, uint32_t tiles_x, uint32_t ntiles,
+                     uint32_t W, uint32_t H, uint32_t *out, hipStream_t st);
+
+}  // namespace rt

@@ -1,4 +1,5 @@
-// rt_device.hip -- gfx950 kernels and the device half of the C-ABI.
+// rt_device.hip -- the device half of the C-ABI: scene upload, renderer state, launches.
+// The kernels live in rt_kernels.inc (built twice: rt_kern_core.hip / rt_kern_ext.hip).
 //
 // Hot path: Renderer::Tick -> Camera::GetPrimaryRay -> Renderer::Trace
 // -> Scene::IntersectBVH / IsOccluded -> Primitive::Intersect / Hit, plus
@@ -29,1170 +30,8 @@
 #include <string>
 #include <vector>
 
+#include "rt_dev_types.h"
 #include "rt_internal.h"
-#include "rt_libm.h"
-
-namespace rt {
-
-enum : uint32_t { T_TRI = 4, T_SPH = 0, T_PLANE = 1, T_CUBE = 2, T_QUAD = 3 };
-enum : int { F_DIFFUSE = 0, F_SPECULAR = 1, F_MIX = 2, F_DIELECTRIC = 3, F_LIGHT = 4 };
-
-struct DevMaterial {
-    int kind, flag;
-    float c0[3], c1[3];
-    float ior, diffuse, specular;
-    uint32_t tex_off, tex_w, tex_h;   // TextureMaterial: texels at SceneView::tex + tex_off
-};
-
-struct SceneView {
-    const float4 *__restrict__ nodes;   // 2 float4 per node
-    const float4 *__restrict__ prims;   // 3 float4 per leaf slot
-    const float4 *__restrict__ shade;   // 2 float4 per primitive id
-    const DevMaterial *__restrict__ mats;
-    const uint32_t *__restrict__ sky;
-    const float4 *__restrict__ xprims;  // cubes / quads: 8 float4 each (Minv rows, M rows, data)
-    const uint32_t *__restrict__ tex;   // all TextureMaterial texels
-    uint32_t sky_w, sky_h;
-    int sky_const;
-    float sky_rgb[3];
-    float light_M[12];                  // prim 0 Transform rows 0..2
-    float light_c[3];
-    float light_r, light_r2, light_invr;
-    int light_mat;
-    int light_quad;                     // prim 0 is a quad (else a sphere)
-    float light_qsize, light_area;      // quad data[0].x; Primitive::GetArea
-    float light_N[3];                   // quad normal TransformVector((0,-1,0), M)
-    uint32_t root_word;
-    int bounds_finite;                  // every node bound is a finite float
-    uint32_t stack_entries;             // LDS stack entries per lane
-    uint32_t node_f4;                   // node array size in float4s
-    int wave_primary;                   // camera rays take the wave-coherent walk
-};
-
-struct FrameArgs {
-    float cam_pos[3], cam_tl[3], cam_tr[3], cam_bl[3];
-    float lens, rw, rh;
-    uint32_t W, H, spp, depth, frame, reset;
-    uint32_t shard, nshards, tiles_x, ntiles_local;
-    int packed_out;
-    float4 *acc;
-    uint32_t *out;
-    unsigned long long *counters;       // [0] shadow rays, [1] bounce rays
-};
-
-struct DRay {
-    f3 O, D, rD;
-    float t;
-    int obj;
-    int inside;
-    float u, v;
-};
-
-__device__ __forceinline__ DRay make_ray(f3 O, f3 D, float t) {   // Ray.h:9-16
-    DRay r;
-    r.O = O; r.D = D; r.t = t; r.obj = -1; r.inside = 0; r.u = 0.0f; r.v = 0.0f;
-    r.rD = mk(1 / D.x, 1 / D.y, 1 / D.z);
-    return r;
-}
-
-// cold-path transcendentals (textured sky, sphere u/v): correctly rounded float via the
-// double functions, as the oracle does; the hot cos/sin/exp come from rt_libm.h
-__device__ __forceinline__ float cr_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
-__device__ __forceinline__ float cr_acos(float x) { return (float)acos((double)x); }
-__device__ __forceinline__ float cr_asin(float x) { return (float)asin((double)x); }
-
-// float -> uint the way the reference's x86-64 build converts: (uint32)(int64)trunc(f)
-__device__ __forceinline__ uint32_t f2u_wrap(float f) {
-    if (!(f == f) || f >= 9.2e18f || f <= -9.2e18f) return 0u;
-    return (uint32_t)(long long)f;
-}
-
-// ------------------------------------------------------------------ slab tests (scene.h:414-450)
-// EXACT: the reference's std::min/std::max selects, NaN behaviour included.
-// FAST (chosen per wave when every active ray has a finite origin and finite 1/D and the
-// scene's node bounds are NaN-free): no slab product can then be NaN, and on non-NaN
-// inputs the selects equal IEEE minNum/maxNum up to the sign of a zero result, which no
-// consumer can observe (the values are only compared) -- so v_min3/v_max3 give the
-// identical decisions with a third of the instructions.
-template <bool FAST>
-__device__ __forceinline__ void slab(const DRay &r, float4 a, float4 b, float &tmn, float &tmx) {
-    float tx1 = (a.x - r.O.x) * r.rD.x, tx2 = (a.w - r.O.x) * r.rD.x;
-    float ty1 = (a.y - r.O.y) * r.rD.y, ty2 = (b.x - r.O.y) * r.rD.y;
-    float tz1 = (a.z - r.O.z) * r.rD.z, tz2 = (b.y - r.O.z) * r.rD.z;
-    if (FAST) {
-        tmn = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-        tmx = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-    } else {
-        tmn = smin(tx1, tx2); tmx = smax(tx1, tx2);
-        tmn = smax(tmn, smin(ty1, ty2)); tmx = smin(tmx, smax(ty1, ty2));
-        tmn = smax(tmn, smin(tz1, tz2)); tmx = smin(tmx, smax(tz1, tz2));
-    }
-}
-template <bool FAST>
-__device__ __forceinline__ float slab_dist(const DRay &r, float4 a, float4 b) {
-    float tmn, tmx;
-    slab<FAST>(r, a, b, tmn, tmx);
-    return (tmx >= tmn && tmn < r.t && tmx > 0) ? tmn : 1e30f;
-}
-template <bool FAST>
-__device__ __forceinline__ bool slab_hit(const DRay &r, float4 a, float4 b) {
-    float tmn, tmx;
-    slab<FAST>(r, a, b, tmn, tmx);
-    return tmx >= tmn && tmn < r.t && tmx > 0;
-}
-__device__ __forceinline__ bool ray_finite(const DRay &r) {
-    return isfinite(r.O.x) && isfinite(r.O.y) && isfinite(r.O.z) && isfinite(r.rD.x) && isfinite(r.rD.y) &&
-           isfinite(r.rD.z);
-}
-
-// ------------------------------------------------------------------ primitive tests (Primitive.h:64-279)
-// TransformPosition / TransformVector with the matrix as three float4 rows (same order of
-// operations as rt_math.h tpos / tvec)
-__device__ __forceinline__ f3 tpos_rows(float4 r0, float4 r1, float4 r2, f3 a) {
-    return mk(r0.x * a.x + r0.y * a.y + r0.z * a.z + r0.w * 1.0f, r1.x * a.x + r1.y * a.y + r1.z * a.z + r1.w * 1.0f,
-              r2.x * a.x + r2.y * a.y + r2.z * a.z + r2.w * 1.0f);
-}
-__device__ __forceinline__ f3 tvec_rows(float4 r0, float4 r1, float4 r2, f3 a) {
-    return mk(r0.x * a.x + r0.y * a.y + r0.z * a.z + r0.w * 0.0f, r1.x * a.x + r1.y * a.y + r1.z * a.z + r1.w * 0.0f,
-              r2.x * a.x + r2.y * a.y + r2.z * a.z + r2.w * 0.0f);
-}
-// CUBE slab test in object space (Primitive.h:87-110 / 196-235); false on a miss
-__device__ __forceinline__ bool cube_slab(const float4 *x, const DRay &r, float &tmin_o, float &tmax_o) {
-    const f3 O = tpos_rows(x[0], x[1], x[2], r.O), D = tvec_rows(x[0], x[1], x[2], r.D);
-    const float4 d0 = x[6], d1 = x[7];
-    const float rDx = 1 / D.x, rDy = 1 / D.y, rDz = 1 / D.z;
-    const bool sx = D.x < 0, sy = D.y < 0, sz = D.z < 0;
-    float tmin = ((sx ? d1.x : d0.x) - O.x) * rDx;
-    float tmax = ((sx ? d0.x : d1.x) - O.x) * rDx;
-    const float tymin = ((sy ? d1.y : d0.y) - O.y) * rDy;
-    const float tymax = ((sy ? d0.y : d1.y) - O.y) * rDy;
-    if (tmin > tymax || tymin > tmax) return false;
-    tmin = smax(tmin, tymin);
-    tmax = smin(tmax, tymax);
-    const float tzmin = ((sz ? d1.z : d0.z) - O.z) * rDz;
-    const float tzmax = ((sz ? d0.z : d1.z) - O.z) * rDz;
-    if (tmin > tzmax || tzmin > tmax) return false;
-    tmin_o = smax(tmin, tzmin);
-    tmax_o = smin(tmax, tzmax);
-    return true;
-}
-// QUAD plane distance in object space (Primitive.h:111-117 / 236-247)
-__device__ __forceinline__ float quad_t(const float4 *x, const DRay &r, f3 &O, f3 &D) {
-    O = tpos_rows(x[0], x[1], x[2], r.O);
-    D = tvec_rows(x[0], x[1], x[2], r.D);
-    return O.y / -D.y;
-}
-// cubes and quads (off the hot path): Intersect; `tie` as in prim_intersect_t
-__device__ __noinline__ void xprim_intersect(const SceneView &S, uint32_t type, uint32_t xi, int id, DRay &r,
-                                             bool &tie) {
-    const float4 *x = S.xprims + 8 * xi;
-    if (type == T_CUBE) {   // the acceptance test is on tmax (Primitive.h:221-233)
-        float tmin, tmax;
-        if (!cube_slab(x, r, tmin, tmax)) return;
-        float t;
-        if (tmin > kEPS) t = tmin;
-        else if (tmax > kEPS) t = tmax;
-        else return;
-        if (tmax < r.t) { r.t = t; r.obj = id; }
-        else if (tmax == r.t) tie = true;
-    } else {
-        f3 O, D;
-        const float t = quad_t(x, r, O, D);
-        const float size = x[6].x;
-        if (t <= r.t && t > kEPS) {
-            const f3 I = O + t * D;
-            if (I.x > -size && I.x < size && I.z > -size && I.z < size) {
-                if (t == r.t) tie = true;
-                else { r.t = t; r.obj = id; r.u = 0.0f; r.v = 0.0f; }   // u, v unset there: 0
-            }
-        }
-    }
-}
-__device__ __noinline__ bool xprim_hit(const SceneView &S, uint32_t type, uint32_t xi, const DRay &r) {
-    const float4 *x = S.xprims + 8 * xi;
-    if (type == T_CUBE) {
-        float tmin, tmax;
-        if (!cube_slab(x, r, tmin, tmax)) return false;
-        return (tmin > kEPS || tmax > kEPS) && tmax < r.t;
-    }
-    f3 O, D;
-    const float t = quad_t(x, r, O, D);   // the quad's extent is not tested (reference quirk)
-    return t < r.t && t > kEPS;
-}
-__device__ __forceinline__ void prim_intersect(const SceneView &S, uint32_t k, DRay &r) {
-    float4 p0 = S.prims[3 * k], p1 = S.prims[3 * k + 1];
-    uint32_t type = __float_as_uint(p1.w);
-    int id = __float_as_int(p0.w);
-    if (type == T_TRI) {
-        float4 p2 = S.prims[3 * k + 2];
-        f3 A = mk(p0.x, p0.y, p0.z), AB = mk(p1.x, p1.y, p1.z), AC = mk(p2.x, p2.y, p2.z);
-        float denom = dot(cross(r.D, AC), AB);
-        if (fabsf(denom) < kDENOM_EPS) return;
-        f3 AO = r.O - A;
-        float u = dot(cross(-r.D, AO), AC) / denom;
-        if (u < 0 || u > 1) return;
-        float v = dot(cross(-r.D, AB), AO) / denom;
-        if (v < 0 || u + v > 1) return;
-        float t = dot(cross(AO, AB), AC) / denom;
-        if (t < r.t && t > kEPS) { r.t = t; r.obj = id; r.u = u; r.v = v; }
-    } else if (type == T_SPH) {
-        f3 oc = r.O - mk(p0.x, p0.y, p0.z);
-        float b = dot(oc, r.D);
-        float c = dot(oc, oc) - p1.x;
-        float d = b * b - c;
-        if (d <= 0) return;
-        d = sqrtf(d);
-        float t = -b - d;
-        if (!(t < r.t && t > kEPS)) {
-            t = d - b;
-            if (!(t < r.t && t > kEPS)) return;
-        }
-        r.t = t; r.obj = id;            // u, v filled in after traversal (finish_uv)
-    } else if (type == T_PLANE) {
-        f3 N = mk(p0.x, p0.y, p0.z);
-        float t = -(dot(r.O, N) + p1.x) / (dot(r.D, N));
-        if (t < r.t && t > kEPS) { r.t = t; r.obj = id; }
-    } else {
-        bool tie = false;
-        xprim_intersect(S, type, __float_as_uint(p1.x), id, r, tie);
-    }
-}
-
-// prim_intersect plus `tie`: set when the candidate distance equals the current r.t
-// exactly (a second primitive at the same distance: the visiting order would decide).
-__device__ __forceinline__ void prim_intersect_t(const SceneView &S, uint32_t k, DRay &r, bool &tie) {
-    float4 p0 = S.prims[3 * k], p1 = S.prims[3 * k + 1];
-    uint32_t type = __float_as_uint(p1.w);
-    int id = __float_as_int(p0.w);
-    if (type == T_TRI) {
-        float4 p2 = S.prims[3 * k + 2];
-        f3 A = mk(p0.x, p0.y, p0.z), AB = mk(p1.x, p1.y, p1.z), AC = mk(p2.x, p2.y, p2.z);
-        float denom = dot(cross(r.D, AC), AB);
-        if (fabsf(denom) < kDENOM_EPS) return;
-        f3 AO = r.O - A;
-        float u = dot(cross(-r.D, AO), AC) / denom;
-        if (u < 0 || u > 1) return;
-        float v = dot(cross(-r.D, AB), AO) / denom;
-        if (v < 0 || u + v > 1) return;
-        float t = dot(cross(AO, AB), AC) / denom;
-        if (t <= r.t && t > kEPS) {
-            if (t == r.t) tie = true;
-            else { r.t = t; r.obj = id; r.u = u; r.v = v; }
-        }
-    } else if (type == T_SPH) {
-        f3 oc = r.O - mk(p0.x, p0.y, p0.z);
-        float b = dot(oc, r.D);
-        float c = dot(oc, oc) - p1.x;
-        float d = b * b - c;
-        if (d <= 0) return;
-        d = sqrtf(d);
-        float t = -b - d;
-        if (t == r.t && t > kEPS) tie = true;
-        if (!(t < r.t && t > kEPS)) {
-            t = d - b;
-            if (t == r.t && t > kEPS) tie = true;
-            if (!(t < r.t && t > kEPS)) return;
-        }
-        r.t = t; r.obj = id;
-    } else if (type == T_PLANE) {
-        f3 N = mk(p0.x, p0.y, p0.z);
-        float t = -(dot(r.O, N) + p1.x) / (dot(r.D, N));
-        if (t == r.t && t > kEPS) tie = true;
-        if (t < r.t && t > kEPS) { r.t = t; r.obj = id; }
-    } else {
-        xprim_intersect(S, type, __float_as_uint(p1.x), id, r, tie);
-    }
-}
-
-__device__ __forceinline__ bool prim_hit(const SceneView &S, uint32_t k, const DRay &r) {
-    float4 p0 = S.prims[3 * k], p1 = S.prims[3 * k + 1];
-    uint32_t type = __float_as_uint(p1.w);
-    if (type == T_TRI) {
-        float4 p2 = S.prims[3 * k + 2];
-        f3 A = mk(p0.x, p0.y, p0.z), AB = mk(p1.x, p1.y, p1.z), AC = mk(p2.x, p2.y, p2.z);
-        float denom = dot(cross(r.D, AC), AB);
-        if (fabsf(denom) < kDENOM_EPS) return false;
-        f3 AO = r.O - A;
-        float u = dot(cross(-r.D, AO), AC) / denom;
-        if (u < 0 || u > 1) return false;
-        float v = dot(cross(-r.D, AB), AO) / denom;
-        if (v < 0 || u + v > 1) return false;
-        float t = dot(cross(AO, AB), AC) / denom;
-        return t < r.t && t > kEPS;
-    } else if (type == T_SPH) {
-        f3 oc = r.O - mk(p0.x, p0.y, p0.z);
-        float b = dot(oc, r.D);
-        float c = dot(oc, oc) - p1.x;
-        float d = b * b - c;
-        if (d <= 0) return false;
-        d = sqrtf(d);
-        float t = -b - d;
-        if (t < r.t && t > kEPS) return true;
-        t = d - b;
-        return t < r.t && t > kEPS;
-    } else if (type == T_PLANE) {
-        f3 N = mk(p0.x, p0.y, p0.z);
-        float t = -(dot(r.O, N) + p1.x) / (dot(r.D, N));
-        return t < r.t && t > kEPS;
-    } else {
-        return xprim_hit(S, type, __float_as_uint(p1.x), r);
-    }
-}
-
-// u, v of a sphere / plane hit, evaluated once for the final hit: identical to the
-// reference's evaluation at acceptance time (same t, same centre).
-__device__ __forceinline__ void finish_uv(const SceneView &S, DRay &r) {
-    if (r.obj < 0) return;
-    float4 s0 = S.shade[2 * r.obj], s1 = S.shade[2 * r.obj + 1];
-    uint32_t type = __float_as_uint(s1.x);
-    f3 I = r.O + r.t * r.D;
-    if (type == T_SPH) {
-        f3 cToI = normalize(I - mk(s0.x, s0.y, s0.z));
-        r.u = 0.5f - cr_atan2(cToI.z, cToI.x) * kINV2PI;
-        r.v = 0.5f - cr_asin(cToI.y) * kINVPI;
-    } else if (type == T_PLANE) {
-        if (s0.x < kFLT_EPSILON && s0.y < kFLT_EPSILON) { r.u = I.x; r.v = -I.y; }
-        else if (s0.x < kFLT_EPSILON && s0.z < kFLT_EPSILON) { r.u = I.x; r.v = -I.z; }
-        else if (s0.y < kFLT_EPSILON && s0.z < kFLT_EPSILON) { r.u = I.y; r.v = -I.z; }
-        else { r.u = 0.0f; r.v = 0.0f; }   // left unset by the reference: defined as 0
-    } else if (type == T_QUAD) {
-        r.u = 0.0f; r.v = 0.0f;
-    } else if (type == T_CUBE) {           // Primitive::setTextureCoordsCube, Primitive.h:752-797
-        const float4 *x = S.xprims + 8 * __float_as_uint(s1.z);
-        const f3 o = tpos_rows(x[0], x[1], x[2], I);
-        const float4 d0 = x[6], d1 = x[7];
-        float uc = o.z, vc = o.y;
-        const float e0 = fabsf(o.x - d0.x), e1 = fabsf(o.x - d1.x), e2 = fabsf(o.y - d0.y), e3 = fabsf(o.y - d1.y);
-        const float e4 = fabsf(o.z - d0.z), e5 = fabsf(o.z - d1.z);
-        float minDist = e0;
-        int face = 1;
-        if (e1 < minDist) uc = -o.z, vc = o.y, face = 0, minDist = e1;
-        if (e2 < minDist) uc = o.x, vc = o.z, face = 3, minDist = e2;
-        if (e3 < minDist) uc = o.x, vc = -o.z, face = 2, minDist = e3;
-        if (e4 < minDist) uc = -o.x, vc = o.y, face = 5, minDist = e4;
-        if (e5 < minDist) uc = o.x, vc = o.y, face = 4;
-        uc = -uc, vc = -vc;
-        uc = 0.5f * (uc / d1.x + 1.0f);
-        vc = 0.5f * (vc / d1.x + 1.0f);
-        const float third = 1.0f / 3.0f;
-        const float fu = face == 0 ? 2.0f : face == 1 ? 0.0f : face == 5 ? 3.0f : 1.0f;
-        const float fv = face == 2 ? 0.0f : face == 3 ? 2.0f : 1.0f;
-        r.u = 0.25f * (fu + uc);
-        r.v = third * (fv + vc);
-    }
-}
-
-// Scene::GetNormal (template/scene.h:489-497) of the hit primitive at I, not yet flipped:
-// Primitive::GetNormal (Primitive.h:284-314)
-__device__ __forceinline__ f3 prim_normal(const SceneView &S, int obj, f3 I) {
-    const float4 s0 = S.shade[2 * obj], s1 = S.shade[2 * obj + 1];
-    const uint32_t type = __float_as_uint(s1.x);
-    if (type == T_SPH) return (I - mk(s0.x, s0.y, s0.z)) * s1.y;
-    if (type != T_CUBE) return mk(s0.x, s0.y, s0.z);
-    const float4 *x = S.xprims + 8 * __float_as_uint(s1.z);
-    const f3 o = tpos_rows(x[0], x[1], x[2], I);
-    const float4 d0 = x[6], d1 = x[7];
-    f3 N = mk(-1, 0, 0);
-    const float e0 = fabsf(o.x - d0.x), e1 = fabsf(o.x - d1.x), e2 = fabsf(o.y - d0.y), e3 = fabsf(o.y - d1.y);
-    const float e4 = fabsf(o.z - d0.z), e5 = fabsf(o.z - d1.z);
-    float minDist = e0;
-    if (e1 < minDist) minDist = e1, N.x = 1;
-    if (e2 < minDist) minDist = e2, N = mk(0, -1, 0);
-    if (e3 < minDist) minDist = e3, N = mk(0, 1, 0);
-    if (e4 < minDist) minDist = e4, N = mk(0, 0, -1);
-    if (e5 < minDist) minDist = e5, N = mk(0, 0, 1);
-    return tvec_rows(x[3], x[4], x[5], N);
-}
-
-// Scene::GetNormal (flipped against the ray) and Scene::GetMaterial of a hit; a
-// TextureMaterial also needs the hit's u, v (deferred by the traversal, finish_uv)
-__device__ __forceinline__ const DevMaterial &hit_surface(const SceneView &S, DRay &ray, f3 I, f3 &N) {
-    N = prim_normal(S, ray.obj, I);
-    if (dot(N, ray.D) > 0) N = -N;
-    const DevMaterial &m = S.mats[__float_as_int(S.shade[2 * ray.obj].w)];
-    if (m.kind == RT_TEXTURE) finish_uv(S, ray);
-    return m;
-}
-
-// ------------------------------------------------------------------ traversal (scene.h:285-320, 452-487)
-// Where a traversal reads its nodes and keeps its stack: `nodes` is the global node array
-// or the workgroup's LDS copy of it; `stk` is this lane's column of the LDS stack, entry i
-// at stk[i * STRIDE] (STRIDE = workgroup size: consecutive lanes, consecutive banks).
-template <int STRIDE>
-struct Trav {
-    const float4 *nodes;
-    uint32_t *stk;
-};
-
-template <bool FAST, int STRIDE>
-__device__ __forceinline__ void closest_hit_t(const SceneView &S, const Trav<STRIDE> &T, DRay &r) {
-    uint32_t *stk = T.stk;
-    uint32_t word = S.root_word;
-    int sp = 0;
-    for (;;) {
-        uint32_t cnt = word & 0xffu, lf = word >> 8;
-        if (cnt) {
-            for (uint32_t k = lf; k < lf + cnt; ++k) prim_intersect(S, k, r);
-            if (sp == 0) break;
-            word = stk[--sp * STRIDE];
-            continue;
-        }
-        const float4 *q = T.nodes + 2 * lf;
-        float4 a0 = q[0], b0 = q[1], a1 = q[2], b1 = q[3];
-        float d1 = slab_dist<FAST>(r, a0, b0), d2 = slab_dist<FAST>(r, a1, b1);
-        uint32_t w1 = __float_as_uint(b0.z), w2 = __float_as_uint(b1.z);
-        if (d1 > d2) { float td = d1; d1 = d2; d2 = td; uint32_t tw = w1; w1 = w2; w2 = tw; }
-        if (d1 == 1e30f) {
-            if (sp == 0) break;
-            word = stk[--sp * STRIDE];
-        } else {
-            word = w1;
-            if (d2 != 1e30f) stk[sp++ * STRIDE] = w2;
-        }
-    }
-}
-
-template <bool FAST, int STRIDE>
-__device__ __forceinline__ bool occluded_t(const SceneView &S, const Trav<STRIDE> &T, const DRay &r) {
-    uint32_t *stk = T.stk;
-    uint32_t word = S.root_word;
-    int sp = 0;
-    for (;;) {
-        uint32_t cnt = word & 0xffu, lf = word >> 8;
-        if (cnt) {
-            for (uint32_t k = lf; k < lf + cnt; ++k)
-                if (prim_hit(S, k, r)) return true;
-            if (sp == 0) return false;
-            word = stk[--sp * STRIDE];
-            continue;
-        }
-        const float4 *q = T.nodes + 2 * lf;
-        float4 a0 = q[0], b0 = q[1], a1 = q[2], b1 = q[3];
-        bool h1 = slab_hit<FAST>(r, a0, b0), h2 = slab_hit<FAST>(r, a1, b1);
-        uint32_t w1 = __float_as_uint(b0.z), w2 = __float_as_uint(b1.z);
-        if (h1 && h2) { word = w1; stk[sp++ * STRIDE] = w2; }
-        else if (!(h1 || h2)) { if (sp == 0) return false; word = stk[--sp * STRIDE]; }
-        else word = h1 ? w1 : w2;
-    }
-}
-
-// ---- wave-coherent closest hit: the calling lanes walk the union of their subtrees with
-// a wave-uniform node and stack (the stack lives in the LDS column of the wave's lane 0 --
-// a VGPR lane-stack cannot be used because the caller may have lanes switched off).
-// Closest hit along the union of the lanes' subtrees; children are visited in the order
-// most calling lanes prefer.  A lane tests a leaf only if its slab test passed with its t
-// at that moment.  Results equal IntersectBVH's whenever the closest hit is unique: `tie`
-// reports a lane that met a second primitive at exactly its current t, and `odd` a hit
-// nearer than its leaf box's entry distance (float rounding at a box face) -- the two
-// ways the visiting order could matter; such lanes are re-traced in the reference order.
-template <int STRIDE>
-__device__ __forceinline__ void wave_closest_hit_fast(const SceneView &S, const Trav<STRIDE> &T, DRay &r, bool &flag) {
-    const float4 *nodes = T.nodes;
-    uint32_t *ws = T.stk - __lane_id();               // the wave's uniform stack (node indices)
-    uint32_t word = __builtin_amdgcn_readfirstlane(S.root_word);
-    bool in = true;
-    float tb = -1e30f;                                // my slab entry distance of the current node
-    uint32_t sp = 0;
-    for (;;) {
-        const uint32_t cnt = word & 0xffu, lf = word >> 8;
-        if (cnt) {
-            if (in)
-                for (uint32_t k = lf; k < lf + cnt; ++k) {
-                    const float t0 = r.t;
-                    prim_intersect_t(S, k, r, flag);
-                    if (r.t != t0 && r.t < tb) flag = true;   // hit nearer than its box's entry
-                }
-        } else {
-            const float4 *q = nodes + 2 * lf;
-            const float4 a0 = q[0], b0 = q[1], a1 = q[2], b1 = q[3];
-            const float d1 = in ? slab_dist<true>(r, a0, b0) : 1e30f, d2 = in ? slab_dist<true>(r, a1, b1) : 1e30f;
-            const bool h1 = d1 != 1e30f, h2 = d2 != 1e30f;
-            const uint64_t m1 = __ballot(h1), m2 = __ballot(h2);
-            if (m1 | m2) {
-                const uint32_t v1 = __popcll(__ballot(h1 && !(h2 && d2 < d1)));
-                const uint32_t v2 = __popcll(__ballot(h2 && !(h1 && d1 <= d2)));
-                const bool first1 = m1 && (!m2 || v1 >= v2);
-                if (m1 && m2) {
-                    ws[sp * STRIDE] = first1 ? lf + 1 : lf;
-                    ++sp;
-                }
-                word = __builtin_amdgcn_readfirstlane(__float_as_uint(first1 ? b0.z : b1.z));
-                in = first1 ? h1 : h2;
-                tb = first1 ? d1 : d2;
-                continue;
-            }
-        }
-        // pop, re-testing each entry with the lanes' current t
-        for (;;) {
-            if (sp == 0) return;
-            --sp;
-            const uint32_t ni = __builtin_amdgcn_readfirstlane(ws[sp * STRIDE]);
-            const float4 a = nodes[2 * ni], b = nodes[2 * ni + 1];
-            tb = slab_dist<true>(r, a, b);
-            in = tb != 1e30f;
-            if (__ballot(in)) {
-                word = __builtin_amdgcn_readfirstlane(__float_as_uint(b.z));
-                break;
-            }
-        }
-    }
-}
-
-template <int STRIDE>
-__device__ __forceinline__ void closest_hit(const SceneView &S, const Trav<STRIDE> &T, DRay &r) {
-    if (__all(S.bounds_finite && ray_finite(r))) closest_hit_t<true>(S, T, r);
-    else closest_hit_t<false>(S, T, r);
-}
-// camera rays: the wave-coherent walk where the scene asks for it (SceneView::wave_primary)
-template <int STRIDE>
-__device__ __forceinline__ void closest_hit_primary(const SceneView &S, const Trav<STRIDE> &T, DRay &r) {
-    if (S.wave_primary && __all(S.bounds_finite && ray_finite(r))) {
-        const DRay r0 = r;
-        bool flag = false;
-        wave_closest_hit_fast(S, T, r, flag);
-        if (flag) { r = r0; closest_hit_t<true>(S, T, r); }
-        return;
-    }
-    closest_hit(S, T, r);
-}
-template <int STRIDE>
-__device__ __forceinline__ bool occluded(const SceneView &S, const Trav<STRIDE> &T, const DRay &r) {
-    if (__all(S.bounds_finite && ray_finite(r))) return occluded_t<true>(S, T, r);
-    return occluded_t<false>(S, T, r);
-}
-
-// ------------------------------------------------------------------ packet traversal (scene.h:322-412)
-// Scene::IntersectBVHPacket with the packet = the wave: lane l holds ray l of the 64-ray
-// packet.  The node, the stack and the "first active" ray are wave-uniform (node and
-// primitive loads are scalar, the stack lives in one VGPR: entry i in lane i); each lane
-// tests its own ray and a ballot finds the lowest hitting lane.  Inactive lanes (past the
-// end of the batch / off screen) never test and never lead.  The VGPR lane-stack needs all
-// 64 lanes switched on: callers invoke it from wave-uniform control flow only.
-__device__ __forceinline__ float readlane_f(float v, uint32_t l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
-}
-
-template <bool FAST>
-__device__ __forceinline__ void packet_closest_hit_t(const SceneView &S, DRay &r, bool active) {
-    const uint32_t lane = __lane_id();
-    uint32_t fa = 0, ni = 0, sp = 0;
-    int stackv = 0;                                   // lane i: stack entry i (node index, depth < 64)
-    for (;;) {
-        ni = __builtin_amdgcn_readfirstlane(ni);
-        const float4 a = S.nodes[2 * ni], b = S.nodes[2 * ni + 1];
-        const uint32_t word = __float_as_uint(b.z), cnt = word & 0xffu, lf = word >> 8;
-        const uint64_t m = __ballot(active && slab_hit<FAST>(r, a, b));
-        uint32_t first = 0;                           // lanes >= first test a leaf
-        bool visit = true;
-        if (!((m >> fa) & 1u)) {
-            if (m == 0) visit = false;
-            else first = fa = (uint32_t)__ffsll((long long)m) - 1u;
-        }
-        if (visit && cnt == 0) {                      // interior: order by the leader's distances
-            const float4 *q = S.nodes + 2 * lf;
-            float d1 = readlane_f(slab_dist<FAST>(r, q[0], q[1]), fa);
-            float d2 = readlane_f(slab_dist<FAST>(r, q[2], q[3]), fa);
-            uint32_t c1 = lf, c2 = lf + 1;
-            if (d1 > d2) { c1 = lf + 1; c2 = lf; }
-            stackv = lane == sp ? (int)c2 : stackv;   // writelane
-            ++sp;
-            ni = c1;
-            continue;
-        }
-        if (visit && active && lane >= first)
-            for (uint32_t k = lf; k < lf + cnt; ++k) prim_intersect(S, k, r);
-        if (sp == 0) break;
-        --sp;
-        ni = (uint32_t)__builtin_amdgcn_readlane(stackv, (int)sp);
-    }
-}
-__device__ __forceinline__ void packet_closest_hit(const SceneView &S, DRay &r, bool active) {
-    if (__all(S.bounds_finite && (!active || ray_finite(r)))) packet_closest_hit_t<true>(S, r, active);
-    else packet_closest_hit_t<false>(S, r, active);
-}
-
-// ------------------------------------------------------------------ shading
-// TEX_SKY = false: every texel is equal (the synthetic sky), so the lookup's index is
-// irrelevant and the colour is the precomputed texel -- bit-identical, no atan2/acos.
-template <bool TEX_SKY>
-__device__ __forceinline__ f3 sky_color(const SceneView &S, f3 D) {   // renderer.h:15-22
-    if (!TEX_SKY) return mk(S.sky_rgb[0], S.sky_rgb[1], S.sky_rgb[2]);
-    uint32_t u = f2u_wrap((float)S.sky_w * cr_atan2(D.z, D.x) * kINV2PI - 0.5f);
-    uint32_t v = f2u_wrap((float)S.sky_h * cr_acos(D.y) * kINVPI - 0.5f);
-    uint32_t p = S.sky[(u & (S.sky_w - 1)) + (v & (S.sky_h - 1)) * S.sky_w];
-    return mk((float)((p >> 16) & 255), (float)((p >> 8) & 255), (float)(p & 255)) * kSKY;
-}
-
-// ObjectMaterial::DiffuseReflection + mapToNormalAxis (ObjectMaterial.h:18-53)
-__device__ __forceinline__ f3 diffuse_dir(f3 N, uint32_t &seed) {
-    float r0 = rnd_f(seed), r1 = rnd_f(seed);
-    float r = sqrtf(r0), theta = kTWOPI * r1;
-    float st, ct;
-    sincos_f(theta, st, ct);
-    float x = r * ct, y = r * st, z = sqrtf(1 - r0);
-    f3 a0 = mk(0.0f, -1.0f, 0.0f), a1 = mk(-1.0f, 0.0f, 0.0f);
-    if (N.z + 1.0f > kFLT_EPSILON) {
-        float a = 1.0f / (1.0f + N.z);
-        float b = -N.x * N.y * a;
-        a0 = mk(1.0f - N.x * N.x * a, b, -N.x);
-        a1 = mk(b, 1.0f - N.y * N.y * a, -N.y);
-    }
-    return normalize(x * a0 + y * a1 + z * N);
-}
-
-__device__ __forceinline__ float fresnel(float n1, float n2, float cost, float cosi) {   // ObjectMaterial.h:55-60
-    float s = (n1 * cosi - n2 * cost) / (n1 * cosi + n2 * cost);
-    float p = (n1 * cost - n2 * cosi) / (n1 * cost + n2 * cosi);
-    return 0.5f * ((s * s) + (p * p));
-}
-
-// ObjectMaterial::scatter overrides.  With last = true the bounce ray is never traced
-// (Trace(.., depth 0) returns 0), so only the RNG draws and the specular flag are kept.
-__device__ __forceinline__ bool scatter(const DevMaterial &m, const DRay &in, f3 I, f3 N, DRay &out, uint32_t &seed,
-                                        bool last) {
-    switch (m.kind) {
-    case RT_DIFFUSE:                                                   // Diffuse.h:16-19
-        if (last) { rnd_u(seed); rnd_u(seed); }
-        else out = make_ray(I, diffuse_dir(N, seed), 1e34f);
-        return false;
-    case RT_MIRROR:                                                    // Mirror.h:16-19
-        if (!last) out = make_ray(I, normalize(reflect(in.D, N)), 1e34f);
-        return true;
-    case RT_DIELECTRIC: {                                              // Dielectric.h:23-54
-        float n1 = 1, n2 = m.ior;
-        float n12 = n1 / n2;
-        float cosi = dot(N, in.D);
-        if (in.inside) n12 = 1 / n12;
-        float k = 1 - (n12 * n12) * (1 - (cosi * cosi));
-        if (k < 0) {
-            if (!last) { out = make_ray(I, normalize(reflect(in.D, N)), 1e34f); out.inside = 1; }
-        } else {
-            float Fr = 0;
-            if (!in.inside) {
-                float sini = length(cross(N, in.D));
-                float sq = n12 * sini;
-                float cost = sqrtf(1 - sq * sq);
-                Fr = fresnel(n1, n2, cost, -cosi);
-            }
-            if (Fr > kFLT_EPSILON && rnd_f(seed) < Fr) {
-                if (!last) out = make_ray(I, normalize(reflect(in.D, N)), 1e34f);
-            } else if (!last) {
-                f3 T = normalize(n12 * in.D - (n12 * cosi + sqrtf(k)) * N);
-                out = make_ray(I, T, 1e34f);
-                out.inside = !in.inside;
-            }
-        }
-        return true;
-    }
-    case RT_LIGHT:
-        return false;
-    default:                                                           // Checkerboard.h:39-58
-        if (m.diffuse < kFLT_EPSILON) {
-            if (!last) out = make_ray(I, normalize(reflect(in.D, N)), 1e34f);
-            return true;
-        }
-        if (m.specular < kFLT_EPSILON) {
-            if (last) { rnd_u(seed); rnd_u(seed); }
-            else out = make_ray(I, diffuse_dir(N, seed), 1e34f);
-            return false;
-        }
-        if (rnd_f(seed) < m.specular) {
-            if (!last) out = make_ray(I, normalize(reflect(in.D, N)), 1e34f);
-            return true;
-        }
-        if (last) { rnd_u(seed); rnd_u(seed); }
-        else out = make_ray(I, diffuse_dir(N, seed), 1e34f);
-        return false;
-    }
-}
-
-// TextureMaterial::GetColor (TextureMaterial.h:30-37); scale = 1/255 (correction) or
-// SKYDOME_CORRECTION (getColorModifier) -- the same float
-__device__ __forceinline__ f3 texture_color(const SceneView &S, const DevMaterial &m, const DRay &in) {
-    const uint32_t u = f2u_wrap((float)m.tex_w * in.u), v = f2u_wrap((float)m.tex_h * in.v);
-    const uint32_t p = S.tex[m.tex_off + (u & (m.tex_w - 1)) + (v & (m.tex_h - 1)) * m.tex_w];
-    return mk((float)((p >> 16) & 255), (float)((p >> 8) & 255), (float)(p & 255)) * (1.0f / 255.0f);
-}
-
-__device__ __forceinline__ f3 mat_color(const SceneView &S, const DevMaterial &m, const DRay &in, f3 I) {
-    if (m.kind == RT_TEXTURE) return texture_color(S, m, in);
-    if (m.kind == RT_DIELECTRIC) {                                     // Dielectric.h:12-21
-        f3 c = mk(1, 1, 1);
-        if (in.inside) { c.x = exp_f(-m.c0[0] * in.t); c.y = exp_f(-m.c0[1] * in.t); c.z = exp_f(-m.c0[2] * in.t); }
-        return c;
-    }
-    if (m.kind == RT_CHECKERBOARD) {                                   // Checkerboard.h:28-37
-        bool ex = abs(((int)floorf(I.x)) % 2) == 0;
-        bool ez = abs(((int)floorf(I.z)) % 2) == 0;
-        return ex == ez ? mk(m.c0[0], m.c0[1], m.c0[2]) : mk(m.c1[0], m.c1[1], m.c1[2]);
-    }
-    return mk(m.c0[0], m.c0[1], m.c0[2]);
-}
-
-// Scene::GetLightPos = Primitive::GetRandomPoint of the light (Primitive.h:394-402, 423-427)
-__device__ __forceinline__ f3 light_point(const SceneView &S, uint32_t &seed) {
-    if (S.light_quad) {   // Primitive.h:423-427: the point lies in object z = 0 (reference quirk)
-        const float a = S.light_qsize * (rnd_f(seed) - 1.0f);
-        const float b = S.light_qsize * (rnd_f(seed) - 1.0f);
-        return tpos(S.light_M, mk(a, b, 0.0f));
-    }
-    f3 pt = mk(1, 1, 1);
-    while (dot(pt, pt) > 1) {
-        float x = rnd_f(seed) * 2.0f - 1.0f;
-        float y = rnd_f(seed) * 2.0f - 1.0f;
-        float z = rnd_f(seed) * 2.0f - 1.0f;
-        pt = mk(x, y, z);
-    }
-    return tpos(S.light_M, normalize(pt) * S.light_r);
-}
-
-// Renderer::NextEventDirectIllumination, renderer.h:44-75 (light = prim 0, a sphere)
-template <int STRIDE>
-__device__ __forceinline__ f3 nee(const SceneView &S, const Trav<STRIDE> &T, f3 I, f3 N, f3 BRDF, uint32_t &seed,
-                                  uint32_t &nshadow) {
-    f3 Il = light_point(S, seed);
-    const float area = S.light_area;                                   // GetArea, Primitive.h:450-468
-    f3 L = Il - I;
-    float dist = length(L);
-    L = L / dist;
-    f3 Nl = S.light_quad ? mk(S.light_N[0], S.light_N[1], S.light_N[2])
-                         : (Il - mk(S.light_c[0], S.light_c[1], S.light_c[2])) * S.light_invr;
-    if (dot(Nl, L) > 0) Nl = -Nl;                                      // Scene::GetNormal flip
-    float dotNL = dot(N, L), dotNlL = dot(Nl, -L);
-    f3 Ld = mk(0, 0, 0);
-    if (dotNL > 0 && dotNlL > 0) {
-        DRay sh = make_ray(I, L, dist - 2.0f * kEPS);
-        ++nshadow;
-        if (!occluded(S, T, sh)) {
-            float solid = (dotNlL * area) / (dist * dist);
-            float lightPDF = 1.0f / solid;
-            const DevMaterial &lm = S.mats[S.light_mat];                // GetLightColor(0, toLight)
-            const f3 lc = lm.kind == RT_LIGHT ? mk(lm.c0[0], lm.c0[1], lm.c0[2]) : mat_color(S, lm, sh, sh.O + sh.t * sh.D);
-            Ld = (lc * BRDF) * (dotNL / lightPDF);
-        }
-    }
-    return Ld;
-}
-
-// Renderer::Trace (renderer.cpp:17-72) as a loop.  The recursion's result
-// BRDF * ((Trace * dot) / PDF) + Ld is folded innermost-first from per-level records,
-// so the float evaluation order is the reference's.
-template <int MAXD, bool TEX_SKY, int STRIDE, bool CAMWAVE = false>
-__device__ f3 trace_path(const SceneView &S, const Trav<STRIDE> &T, DRay ray, int depth, uint32_t &seed,
-                         uint32_t &nshadow, uint32_t &nbounce, bool lastSpec = true) {
-    f3 lv_mul[MAXD], lv_add[MAXD];
-    float lv_c[MAXD];
-    bool lv_diff[MAXD];
-    int levels = 0;
-    f3 term = mk(0, 0, 0);
-    for (int d = depth; d > 0 && levels < MAXD; --d) {
-        if (d != depth) ++nbounce;
-        if (CAMWAVE && d == depth) closest_hit_primary(S, T, ray);
-        else closest_hit(S, T, ray);
-        if (ray.obj == -1) { term = sky_color<TEX_SKY>(S, ray.D); break; }
-        f3 I = ray.O + ray.t * ray.D;
-        f3 N;
-        const DevMaterial &m = hit_surface(S, ray, I, N);
-        if (m.flag == F_LIGHT) { term = lastSpec ? mk(m.c0[0], m.c0[1], m.c0[2]) : mk(0, 0, 0); break; }
-        const bool last = MAXD == 1 || d == 1;   // MAXD 1: the bounce ray is never traced
-        DRay out;
-        bool spec = scatter(m, ray, I, N, out, seed, last);
-        f3 albedo = mat_color(S, m, ray, I);
-        if (m.flag == F_DIFFUSE || (m.flag == F_MIX && !spec)) {
-            f3 BRDF = albedo * kINVPI;
-            lv_add[levels] = nee(S, T, I, N, BRDF, seed, nshadow);
-            lv_mul[levels] = BRDF;
-            lv_c[levels] = last ? 0.0f : dot(N, out.D);
-            lv_diff[levels] = true;
-        } else {
-            lv_mul[levels] = albedo;
-            lv_add[levels] = mk(0, 0, 0);
-            lv_c[levels] = 0.0f;
-            lv_diff[levels] = false;
-        }
-        ++levels;
-        if (last) break;
-        ray = out;
-        lastSpec = spec;
-    }
-    f3 r = term;
-    for (int k = levels - 1; k >= 0; --k)
-        r = lv_diff[k] ? lv_mul[k] * ((r * lv_c[k]) / kINV2PI) + lv_add[k] : lv_mul[k] * r;
-    return r;
-}
-
-// Renderer::TracePacket's per-ray shading (renderer.cpp:78-133): the primary hit comes
-// from the packet traversal, every bounce is a Trace(ray_out, specularBounce, depth).
-template <int MAXD, bool TEX_SKY, int STRIDE>
-__device__ f3 shade_packet(const SceneView &S, const Trav<STRIDE> &T, DRay ray, int depth, uint32_t &seed,
-                           uint32_t &nshadow, uint32_t &nbounce) {
-    if (ray.obj == -1) return sky_color<TEX_SKY>(S, ray.D);
-    f3 I = ray.O + ray.t * ray.D;
-    f3 N;
-    const DevMaterial &m = hit_surface(S, ray, I, N);
-    const bool last = depth == 0;                  // Trace(.., 0) returns 0: the bounce is never traced
-    DRay out;
-    bool spec = scatter(m, ray, I, N, out, seed, last);
-    f3 albedo = mat_color(S, m, ray, I);
-    if (m.flag == F_LIGHT) return albedo;
-    const bool diffuse = m.flag == F_DIFFUSE || m.flag == F_MIX;
-    // MIX + specular bounce: the ray is traced for a result that is then overwritten
-    // (renderer.cpp:111-114) and traced again after NEE (116-120).  One call site.
-    const int passes = (m.flag == F_MIX && spec) ? 2 : 1;
-    const f3 BRDF = albedo * kINVPI;
-    f3 Ld = mk(0, 0, 0), Li = mk(0, 0, 0);
-    for (int p = 0; p < passes; ++p) {
-        if (diffuse && p == passes - 1) Ld = nee(S, T, I, N, BRDF, seed, nshadow);
-        nbounce += last ? 0u : 1u;
-        Li = trace_path<MAXD, TEX_SKY>(S, T, out, depth, seed, nshadow, nbounce, spec);
-    }
-    if (!diffuse) return albedo * Li;
-    f3 Ei = (Li * (last ? 0.0f : dot(N, out.D))) / kINV2PI;
-    return BRDF * Ei + Ld;
-}
-
-// ------------------------------------------------------------------ Whitted (the K key)
-// ObjectMaterial::getColorModifier overrides: colour in c, colorVars[3] in c3 and the
-// refraction direction colorVars[4..6] in T (Diffuse.h:21-23, Mirror.h:21-23,
-// Light.h:20-22, Checkerboard.h:60-71, Dielectric.h:56-85).
-__device__ __forceinline__ void color_modifier(const SceneView &S, const DevMaterial &m, const DRay &in, f3 I, f3 N, f3 &c, float &c3,
-                                               f3 &T) {
-    c3 = 0.0f;
-    T = mk(0, 0, 0);
-    switch (m.kind) {
-    case RT_LIGHT:   // clamp = fmaxf(a, fminf(f, b)), template/precomp.h:782
-        c = mk(fmaxf(0.0f, fminf(m.c0[0], 1.0f)), fmaxf(0.0f, fminf(m.c0[1], 1.0f)), fmaxf(0.0f, fminf(m.c0[2], 1.0f)));
-        return;
-    case RT_CHECKERBOARD:
-    case RT_TEXTURE:                 // TextureMaterial.h:62-71
-        c = mat_color(S, m, in, I);
-        c3 = m.diffuse;
-        return;
-    case RT_DSMIX:                   // DSMix.h:48-50
-        c = mk(m.c0[0], m.c0[1], m.c0[2]);
-        c3 = m.diffuse;
-        return;
-    case RT_DIELECTRIC: {
-        float n1 = 1, n2 = m.ior, n12 = n1 / n2;
-        float cosi = dot(N, in.D);
-        c = mk(1, 1, 1);
-        if (in.inside) {
-            c = mk(exp_f(-m.c0[0] * in.t), exp_f(-m.c0[1] * in.t), exp_f(-m.c0[2] * in.t));
-            n12 = 1 / n12;
-        }
-        float k = 1 - (n12 * n12) * (1 - (cosi * cosi));
-        if (k < 0) { c3 = -1.0f; return; }   // TIR
-        if (!in.inside) {
-            float sini = length(cross(N, in.D));
-            float sq = n12 * sini;
-            float cost = sqrtf(1 - sq * sq);
-            c3 = fresnel(n1, n2, cost, -cosi);
-        }
-        T = normalize(n12 * in.D - (n12 * cosi + sqrtf(k)) * N);
-        return;
-    }
-    default:
-        c = mk(m.c0[0], m.c0[1], m.c0[2]);
-        return;
-    }
-}
-
-// Renderer::DirectIllumination, renderer.h:24-42: 4 light-sphere samples, spotlight test
-// against GetLightDir (0,-1,0), GetLightColor (24,24,22) (template/scene.h:234-242).
-template <int STRIDE>
-__device__ __forceinline__ f3 direct_illumination(const SceneView &S, const Trav<STRIDE> &T, f3 I, f3 N,
-                                                  uint32_t &seed, uint32_t &nshadow) {
-    f3 result = mk(0, 0, 0);
-    const f3 ldir = mk(0.0f, -1.0f, 0.0f), lcol = mk(24.0f, 24.0f, 22.0f);
-    for (int i = 0; i < 4; ++i) {
-        f3 L = light_point(S, seed) - I;
-        float dist = length(L);
-        L = L / dist;
-        float dotDN = dot(L, N);
-        if (dotDN < 0 || dot(ldir, L) > 0) continue;
-        DRay sh = make_ray(I, L, dist - (2 * kEPS));
-        ++nshadow;
-        if (occluded(S, T, sh)) continue;
-        result = result + (dotDN / (dist * dist)) * lcol;
-    }
-    return result / 4.0f;
-}
-
-// Renderer::WhittedTrace (renderer.cpp:138-195) as a depth-first walk with an explicit
-// frame stack.  A frame holds the parent's colour modifier and its partial sum; a child's
-// value is added (scaled by Fr, Ft or 1 - diffuse) when it returns, and the dielectric's
-// refraction child starts only after the reflection child is finished -- the reference's
-// evaluation and RNG order, so results are bit-identical to the recursion.
-constexpr int kWHITTED_MAX = 32;
-struct WFrame {
-    f3 col, res, I, T;
-    float w, ft;
-    int flags;   // 1: scale the child by w, 2: refraction child pending, 4: its inside flag
-};
-
-template <bool TEX_SKY, int STRIDE>
-__device__ f3 trace_whitted(const SceneView &S, const Trav<STRIDE> &T, DRay ray, int depth, uint32_t &seed,
-                            uint32_t &nshadow, uint32_t &nbounce) {
-    WFrame st[kWHITTED_MAX];
-    int sp = 0;
-    bool primary = true;
-    for (;;) {
-        // ---- evaluate WhittedTrace(ray, depth - sp) up to its first child
-        f3 ret = mk(0, 0, 0);
-        if (depth - sp > 0) {
-            if (!primary) ++nbounce;
-            primary = false;
-            closest_hit(S, T, ray);
-            if (ray.obj == -1) {
-                ret = sky_color<TEX_SKY>(S, ray.D);
-            } else {
-                f3 I = ray.O + ray.t * ray.D;
-                f3 N;
-                const DevMaterial &m = hit_surface(S, ray, I, N);
-                f3 col, Tdir;
-                float c3;
-                color_modifier(S, m, ray, I, N, col, c3, Tdir);
-                f3 res = mk(0, 0, 0);
-                WFrame f;
-                f.col = col; f.w = 1.0f; f.ft = 0.0f; f.flags = 0;
-                bool push = false, child_inside = false;
-                f3 childD = mk(0, 0, 0);
-                if (m.flag == F_LIGHT) {
-                    res = res + mk(24.0f, 24.0f, 22.0f);
-                } else if (m.flag == F_DIFFUSE) {
-                    res = res + direct_illumination(S, T, I, N, seed, nshadow);
-                } else if (m.flag == F_SPECULAR) {
-                    push = true; childD = normalize(reflect(ray.D, N));
-                } else if (m.flag == F_MIX) {
-                    res = res + c3 * direct_illumination(S, T, I, N, seed, nshadow);
-                    push = true; childD = normalize(reflect(ray.D, N));
-                    f.w = 1.0f - c3; f.flags = 1;
-                } else if (m.flag == F_DIELECTRIC) {
-                    if (c3 < 0) {
-                        push = true; childD = normalize(reflect(ray.D, N)); child_inside = true;
-                    } else {
-                        float Fr = c3, Ft = 1 - Fr;
-                        if (Fr > kFLT_EPSILON) {
-                            push = true; childD = normalize(reflect(ray.D, N));
-                            f.w = Fr; f.flags = 1;
-                            if (Ft > kFLT_EPSILON) {
-                                f.flags |= 2 | (ray.inside ? 0 : 4);
-                                f.ft = Ft; f.I = I; f.T = Tdir;
-                            }
-                        } else if (Ft > kFLT_EPSILON) {
-                            push = true; childD = Tdir; child_inside = !ray.inside;
-                            f.w = Ft; f.flags = 1;
-                        }
-                    }
-                }
-                if (push) {
-                    f.res = res;
-                    st[sp++] = f;
-                    ray = make_ray(I, childD, 1e34f);
-                    ray.inside = child_inside ? 1 : 0;
-                    continue;
-                }
-                ret = col * res;
-            }
-        }
-        // ---- return ret to the parents until one has a child left to trace
-        bool descend = false;
-        while (sp > 0) {
-            WFrame &f = st[sp - 1];
-            f.res = f.res + ((f.flags & 1) ? f.w * ret : ret);
-            if (f.flags & 2) {
-                ray = make_ray(f.I, f.T, 1e34f);
-                ray.inside = (f.flags & 4) ? 1 : 0;
-                f.w = f.ft;
-                f.flags &= ~2;
-                descend = true;
-                break;
-            }
-            ret = f.col * f.res;
-            --sp;
-        }
-        if (!descend) return ret;
-    }
-}
-
-// Camera::GetPrimaryRay (camera.h:43-52) + randomInUnitDisk (20-26)
-__device__ __forceinline__ DRay primary_ray(const FrameArgs &F, uint32_t x, uint32_t y, uint32_t &seed) {
-    float u = (float)x * F.rw + rnd_f(seed) * F.rw;
-    float v = (float)y * F.rh + rnd_f(seed) * F.rh;
-    f3 p;
-    for (;;) {
-        float px = rnd_f(seed) * 2.0f - 1.0f;
-        float py = rnd_f(seed) * 2.0f - 1.0f;
-        p = mk(px, py, 0);
-        if (!(dot(p, p) >= 1)) break;
-    }
-    f3 rd = F.lens * p;
-    f3 offset = mk(u * rd.x, v * rd.y, 0);
-    f3 pos = mk(F.cam_pos[0], F.cam_pos[1], F.cam_pos[2]);
-    f3 tl = mk(F.cam_tl[0], F.cam_tl[1], F.cam_tl[2]);
-    f3 tr = mk(F.cam_tr[0], F.cam_tr[1], F.cam_tr[2]);
-    f3 bl = mk(F.cam_bl[0], F.cam_bl[1], F.cam_bl[2]);
-    f3 P = tl + u * (tr - tl) + v * (bl - tl);
-    return make_ray(pos + offset, normalize(P - pos - offset), 1e34f);
-}
-
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// RGBF32_to_RGB8, template/precomp.h:441-444
-__device__ __forceinline__ uint32_t pack_rgb8(float4 a) {
-    uint32_t r = f2u_wrap(255.0f * smin(1.0f, a.x));
-    uint32_t g = f2u_wrap(255.0f * smin(1.0f, a.y));
-    uint32_t b = f2u_wrap(255.0f * smin(1.0f, a.z));
-    return (r << 16) + (g << 8) + b;
-}
-
-// ------------------------------------------------------------------ kernels
-// One screen tile (8x8, one wave) of one frame: per pixel spp x Trace / WhittedTrace /
-// TracePacket (the tile is the packet, renderer.cpp:247-285), running average into the
-// accumulator (renderer.cpp:235-241), RGB8 pack; per-wave ray counters.
-enum : int { M_PATH = RT_MODE_PATH, M_WHITTED = RT_MODE_WHITTED, M_PACKET = RT_MODE_PACKET };
-
-template <int MODE, int MAXD, bool TEX_SKY, int STRIDE>
-__device__ __forceinline__ void render_tile(const SceneView &S, const FrameArgs &F, const Trav<STRIDE> &T,
-                                            uint32_t local_tile, uint32_t lane) {
-    const uint32_t tile = local_tile * F.nshards + F.shard;
-    const uint32_t x = (tile % F.tiles_x) * 8u + (lane & 7u), y = (tile / F.tiles_x) * 8u + (lane >> 3);
-    const bool on = x < F.W && y < F.H;
-    const uint32_t px = x + y * F.W;
-    // the wave-coherent camera-ray walk is compiled into the global-node primary+shadow
-    // kernel only (SceneView::wave_primary picks it at run time)
-    constexpr bool kCamWave = MODE == M_PATH && MAXD == 1 && STRIDE == 256;
-    uint32_t nshadow = 0, nbounce = 0;
-    f3 sum = mk(0, 0, 0);
-    if (MODE == M_PACKET) {                           // the traversal is wave-wide: no early exit
-        for (uint32_t s = 0; s < F.spp; ++s) {
-            uint32_t seed = init_seed(px + F.W * F.H * (s + F.spp * F.frame));
-            DRay ray = on ? primary_ray(F, x, y, seed) : make_ray(mk(0, 0, 0), mk(0, 0, 1), 1e34f);
-            packet_closest_hit(S, ray, on);
-            if (on) sum = sum + shade_packet<MAXD, TEX_SKY>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
-        }
-    } else if (on) {
-        for (uint32_t s = 0; s < F.spp; ++s) {
-            uint32_t seed = init_seed(px + F.W * F.H * (s + F.spp * F.frame));
-            DRay ray = primary_ray(F, x, y, seed);
-            if constexpr (MODE == M_WHITTED) sum = sum + trace_whitted<TEX_SKY>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
-            else sum = sum + trace_path<MAXD, TEX_SKY, STRIDE, kCamWave>(S, T, ray, (int)F.depth, seed, nshadow, nbounce);
-        }
-    }
-    if (on) {
-        f3 res = (1.0f / (float)F.spp) * sum;
-        float4 a = F.reset ? make_float4(0, 0, 0, 0) : F.acc[px];
-        a.w += 1;                                                      // renderer.cpp:237-240
-        const float w = a.w, inv = 1.0f / w;
-        a = make_float4(a.x + inv * (res.x - a.x), a.y + inv * (res.y - a.y), a.z + inv * (res.z - a.z),
-                        a.w + inv * (w - a.w));
-        F.acc[px] = a;
-        const uint32_t rgb = pack_rgb8(a);
-        if (F.packed_out) F.out[local_tile * 64u + lane] = rgb;
-        else F.out[px] = rgb;
-    }
-    nshadow = wave_sum(nshadow);
-    nbounce = wave_sum(nbounce);
-    if (lane == 0) {
-        if (nshadow) atomicAdd(&F.counters[0], (unsigned long long)nshadow);
-        if (nbounce) atomicAdd(&F.counters[1], (unsigned long long)nbounce);
-    }
-}
-
-// Global-node variant: 256-thread workgroups, wave w of workgroup b owns local tile b*4+w.
-#ifndef RT_RENDER_WAVES_PER_SIMD
-#define RT_RENDER_WAVES_PER_SIMD 1
-#endif
-template <int MODE, int MAXD, bool TEX_SKY>
-__global__ __launch_bounds__(256, RT_RENDER_WAVES_PER_SIMD) void k_render(SceneView S, FrameArgs F) {
-    extern __shared__ uint32_t lds_stack[];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t local_tile = blockIdx.x * 4u + (tid >> 6);
-    if (local_tile >= F.ntiles_local) return;
-    Trav<256> T{S.nodes, lds_stack + tid};
-    render_tile<MODE, MAXD, TEX_SKY>(S, F, T, local_tile, tid & 63u);
-}
-
-// LDS-node variant for scenes whose node array fits beside the stacks (TEAPOT-F: 65 KB):
-// a 1024-thread workgroup copies the node array into LDS, then its 16 waves render 16
-// consecutive tiles (a 128x8 strip) reading every 64-byte sibling pair with ds_read_b128
-// instead of a vector-memory load.  One strip per workgroup leaves the balancing across
-// CUs to the hardware dispatcher: persistent grids with static or per-CU queues measured
-// 5-13 % slower (profiles/r01/ab_lds_*.json).  LDS = [stack_entries][1024] u32 | nodes.
-template <int MAXD, bool TEX_SKY>
-__global__ __launch_bounds__(1024) void k_render_lds(SceneView S, FrameArgs F) {
-    extern __shared__ uint32_t lds[];
-    const uint32_t tid = threadIdx.x;
-    float4 *lnodes = reinterpret_cast<float4 *>(lds + S.stack_entries * 1024u);
-    for (uint32_t i = tid; i < S.node_f4; i += 1024u) lnodes[i] = S.nodes[i];
-    __syncthreads();
-    const uint32_t local_tile = blockIdx.x * 16u + (tid >> 6);
-    if (local_tile >= F.ntiles_local) return;
-    Trav<1024> T{lnodes, lds + tid};
-    render_tile<M_PATH, MAXD, TEX_SKY>(S, F, T, local_tile, tid & 63u);
-}
-
-__global__ __launch_bounds__(256) void k_intersect(SceneView S, const rt_ray *__restrict__ rays, rt_hit *__restrict__ hits,
-                                                   uint32_t n) {
-    extern __shared__ uint32_t lds_stack[];
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= n) return;
-    rt_ray q = rays[i];
-    DRay r = make_ray(mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), q.tmax);
-    Trav<256> T{S.nodes, lds_stack + threadIdx.x};
-    closest_hit(S, T, r);
-    finish_uv(S, r);
-    rt_hit h;
-    h.t = r.t; h.obj = r.obj; h.u = r.u; h.v = r.v;
-    hits[i] = h;
-}
-
-// batched Scene::IntersectBVHPacket: wave w traces rays [64w, 64w + 64) as one packet
-__global__ __launch_bounds__(256) void k_intersect_packet(SceneView S, const rt_ray *__restrict__ rays,
-                                                          rt_hit *__restrict__ hits, uint32_t n) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if ((i & ~63u) >= n) return;                      // whole waves only
-    const bool active = i < n;
-    DRay r = make_ray(mk(0, 0, 0), mk(0, 0, 1), 1e34f);
-    if (active) {
-        rt_ray q = rays[i];
-        r = make_ray(mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), q.tmax);
-    }
-    packet_closest_hit(S, r, active);
-    if (!active) return;
-    finish_uv(S, r);
-    rt_hit h;
-    h.t = r.t; h.obj = r.obj; h.u = r.u; h.v = r.v;
-    hits[i] = h;
-}
-
-__global__ __launch_bounds__(256) void k_occluded(SceneView S, const rt_ray *__restrict__ rays, uint8_t *__restrict__ out,
-                                                  uint32_t n) {
-    extern __shared__ uint32_t lds_stack[];
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= n) return;
-    rt_ray q = rays[i];
-    DRay r = make_ray(mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), q.tmax);
-    Trav<256> T{S.nodes, lds_stack + threadIdx.x};
-    out[i] = occluded(S, T, r) ? 1 : 0;
-}
-
-// rank-0 side of the per-frame gather: packed shard tiles -> row-major frame
-__global__ __launch_bounds__(256) void k_assemble(const uint32_t *__restrict__ gathered, uint32_t cap, uint32_t nshards,
-                                                  uint32_t tiles_x, uint32_t ntiles, uint32_t W, uint32_t H,
-                                                  uint32_t *__restrict__ out) {
-    const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    if (tile >= ntiles) return;
-    const uint32_t x = (tile % tiles_x) * 8u + (lane & 7u), y = (tile / tiles_x) * 8u + (lane >> 3);
-    if (x >= W || y >= H) return;
-    const uint32_t shard = tile % nshards, local = tile / nshards;
-    out[x + y * W] = gathered[(size_t)shard * cap + local * 64u + lane];
-}
-
-}  // namespace rt
 
 // ====================================================================== host side
 using namespace rt;
@@ -1215,8 +54,9 @@ struct rt_scene {
     bool lds_nodes = false;     // frame kernel keeps the node array in LDS (k_render_lds)
     uint32_t num_cus = 256;     // persistent grid size of k_render_lds
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
+    bool ext = false;           // needs the kext kernels (cubes, quads, textures, non-Light light)
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
-    void *d_xprims = nullptr, *d_tex = nullptr;
+    void *d_xprims = nullptr, *d_tex = nullptr, *d_pairs = nullptr;
     void *d_scratch = nullptr;  // staging for the host-pointer batched calls
     size_t scratch_bytes = 0;
     hipStream_t stream = nullptr;
@@ -1286,7 +126,8 @@ void free_scene(rt_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     (void)hipDeviceSynchronize();
-    void *ptrs[] = {s->d_nodes, s->d_prims, s->d_shade, s->d_mats, s->d_sky, s->d_xprims, s->d_tex, s->d_scratch};
+    void *ptrs[] = {s->d_nodes, s->d_pairs, s->d_prims, s->d_shade, s->d_mats, s->d_sky, s->d_xprims, s->d_tex,
+                    s->d_scratch};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -1338,6 +179,13 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     for (uint32_t i = 0; i < d->num_textures; ++i)
         if (!d->textures[i].pixels || !d->textures[i].width || !d->textures[i].height)
             return fail(RT_ERR_INVALID, "texture " + std::to_string(i) + " is empty");
+    bool ext = d->prims[0].type == RT_QUAD;
+    {
+        const int lk = d->materials[d->prims[0].material].kind;
+        ext = ext || !(lk == RT_LIGHT || lk == RT_DIFFUSE || lk == RT_MIRROR || lk == RT_DSMIX);
+    }
+    for (uint32_t i = 0; i < n && !ext; ++i) ext = d->prims[i].type == RT_CUBE || d->prims[i].type == RT_QUAD;
+    for (uint32_t i = 0; i < d->num_materials && !ext; ++i) ext = d->materials[i].kind == RT_TEXTURE;
     if (d->sky_pixels) {
         uint32_t w = d->sky_width, h = d->sky_height;
         if (!w || !h || (w & (w - 1)) || (h & (h - 1)))
@@ -1348,6 +196,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 
     rt_scene *s = new rt_scene();
     s->device = d->device;
+    s->ext = ext;
     s->num_prims = n;
     // ---- BVH: prebuilt (validated) or built here
     if (d->bvh_nodes) {
@@ -1387,6 +236,17 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         uint32_t word = (nd.leftFirst << 8) | nd.count;
         nodes[2 * i] = make_float4(nd.mn[0], nd.mn[1], nd.mn[2], nd.mx[0]);
         nodes[2 * i + 1] = make_float4(nd.mx[1], nd.mx[2], ubits(word), 0.0f);
+    }
+    // ---- the same nodes as interleaved child pairs for the LDS kernel: pair k = nodes
+    // (2k, 2k+1) at float4 4k: X = (mn.x, mn.x', mx.x, mx.x'), Y, Z alike, then the words
+    std::vector<float4> pairs(nodes.size(), make_float4(0, 0, 0, 0));
+    for (uint32_t k = 1; 2 * k + 1 < s->bvh.nodes_used; ++k) {
+        const Node &a = s->bvh.nodes[2 * k], &b = s->bvh.nodes[2 * k + 1];
+        const uint32_t wa = (a.leftFirst << 8) | a.count, wb = (b.leftFirst << 8) | b.count;
+        pairs[4 * k + 0] = make_float4(a.mn[0], b.mn[0], a.mx[0], b.mx[0]);
+        pairs[4 * k + 1] = make_float4(a.mn[1], b.mn[1], a.mx[1], b.mx[1]);
+        pairs[4 * k + 2] = make_float4(a.mn[2], b.mn[2], a.mx[2], b.mx[2]);
+        pairs[4 * k + 3] = make_float4(ubits(wa), ubits(wb), 0.0f, 0.0f);
     }
     // ---- leaf-order primitive records and per-id shading records; cubes and quads keep
     // their matrices and data in a side table (8 float4 each)
@@ -1510,6 +370,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 
     rc = RT_OK;
     if (rc == RT_OK) rc = upload(&s->d_nodes, nodes);
+    if (rc == RT_OK) rc = upload(&s->d_pairs, pairs);
     if (rc == RT_OK) rc = upload(&s->d_prims, prims);
     if (rc == RT_OK) rc = upload(&s->d_shade, shade);
     if (rc == RT_OK) rc = upload(&s->d_mats, mats);
@@ -1522,6 +383,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 
     SceneView &v = s->view;
     v.nodes = (const float4 *)s->d_nodes;
+    v.pairs = (const float4 *)s->d_pairs;
     v.prims = (const float4 *)s->d_prims;
     v.shade = (const float4 *)s->d_shade;
     v.mats = (const DevMaterial *)s->d_mats;
@@ -1635,31 +497,9 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         block = dim3(256);
         lds = stack_bytes(s);
     }
-#define RT_LAUNCH(MO, MD, TX) hipLaunchKernelGGL((k_render<MO, MD, TX>), grid, block, lds, st, s->view, F)
-    if (use_lds) hipLaunchKernelGGL((k_render_lds<1, false>), grid, block, lds, st, s->view, F);
-    else if (mode == RT_MODE_WHITTED) {
-        if (tex) RT_LAUNCH(M_WHITTED, 1, true); else RT_LAUNCH(M_WHITTED, 1, false);
-    } else if (mode == RT_MODE_PACKET) {                // depth = the bounces' Trace depth (0 allowed)
-        const int pd = depth <= 1 ? 1 : depth <= 10 ? 10 : 32;
-        switch (pd * 2 + (tex ? 1 : 0)) {
-        case 2: RT_LAUNCH(M_PACKET, 1, false); break;
-        case 3: RT_LAUNCH(M_PACKET, 1, true); break;
-        case 20: RT_LAUNCH(M_PACKET, 10, false); break;
-        case 21: RT_LAUNCH(M_PACKET, 10, true); break;
-        case 64: RT_LAUNCH(M_PACKET, 32, false); break;
-        default: RT_LAUNCH(M_PACKET, 32, true); break;
-        }
-    } else switch (md * 2 + (tex ? 1 : 0)) {
-    case 2: RT_LAUNCH(M_PATH, 1, false); break;
-    case 3: RT_LAUNCH(M_PATH, 1, true); break;
-    case 8: RT_LAUNCH(M_PATH, 4, false); break;
-    case 9: RT_LAUNCH(M_PATH, 4, true); break;
-    case 20: RT_LAUNCH(M_PATH, 10, false); break;
-    case 21: RT_LAUNCH(M_PATH, 10, true); break;
-    case 64: RT_LAUNCH(M_PATH, 32, false); break;
-    default: RT_LAUNCH(M_PATH, 32, true); break;
-    }
-#undef RT_LAUNCH
+FrameLaunch L{mode, md, tex, use_lds, grid, block, lds, st};
+    if (s->ext) kext::launch_frame(s->view, F, L);
+    else kcore::launch_frame(s->view, F, L);
     HIP_TRY(hipGetLastError());
     // pixels covered by this launch (primary rays per sample)
     uint64_t px = (uint64_t)F.ntiles_local * 64u;
@@ -1751,7 +591,8 @@ int rt_intersect(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t n, void
     if (n == 0) return RT_OK;
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_intersect, dim3((n + 255) / 256), dim3(256), stack_bytes(s), st, s->view, rays, hits, n);
+    if (s->ext) kext::launch_intersect(s->view, rays, hits, n, stack_bytes(s), st);
+    else kcore::launch_intersect(s->view, rays, hits, n, stack_bytes(s), st);
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }
@@ -1761,7 +602,8 @@ int rt_occluded(rt_scene *s, const rt_ray *rays, uint8_t *out, uint32_t n, void 
     if (n == 0) return RT_OK;
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_occluded, dim3((n + 255) / 256), dim3(256), stack_bytes(s), st, s->view, rays, out, n);
+    if (s->ext) kext::launch_occluded(s->view, rays, out, n, stack_bytes(s), st);
+    else kcore::launch_occluded(s->view, rays, out, n, stack_bytes(s), st);
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }
@@ -1771,7 +613,8 @@ int rt_intersect_packets(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t
     if (n == 0) return RT_OK;
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_intersect_packet, dim3((n + 255) / 256), dim3(256), 0, st, s->view, rays, hits, n);
+    if (s->ext) kext::launch_intersect_packet(s->view, rays, hits, n, st);
+    else kcore::launch_intersect_packet(s->view, rays, hits, n, st);
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }
@@ -1880,8 +723,7 @@ int rt_assemble_shards(rt_renderer *r, const uint32_t *gathered, uint32_t nshard
     rt_shard_capacity(r->W, r->H, nshards, &cap);
     uint32_t tiles_x = (r->W + 7) / 8, ntiles = tiles_x * ((r->H + 7) / 8);
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_assemble, dim3((ntiles + 3) / 4), dim3(256), 0, st, gathered, cap, nshards, tiles_x, ntiles,
-                       r->W, r->H, rgb8);
+    launch_assemble(gathered, cap, nshards, tiles_x, ntiles, r->W, r->H, rgb8, st);
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }

@@ -1,11 +1,10 @@
 #!/bin/bash
-# build_variant.sh NAME [DEVICE_SRC] [extra hipcc flags...] -> variants/NAME.so
+# build_variant.sh NAME [extra hipcc flags...] -> variants/NAME.so (for tools/ab.py A/B runs)
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
-src=advancedgraphicsraytracer_amd/csrc/rt_device.hip
-if [ $# -gt 0 ] && [ -f "$1" ]; then src=$1; shift; fi
 mkdir -p variants
+C=advancedgraphicsraytracer_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -Wno-unused-function \
-  -I advancedgraphicsraytracer_amd/csrc "$@" -o variants/$name.so advancedgraphicsraytracer_amd/csrc/rt_host.cpp "$src" -lz
+  -I $C "$@" -o variants/$name.so -x hip $C/rt_host.cpp $C/rt_device.hip $C/rt_kern_core.hip $C/rt_kern_ext.hip -lz
 echo variants/$name.so

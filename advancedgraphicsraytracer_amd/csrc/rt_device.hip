@@ -33,6 +33,7 @@
 #include "rt_dev_types.h"
 #include "rt_internal.h"
 
+
 // ====================================================================== host side
 using namespace rt;
 
@@ -497,7 +498,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         block = dim3(256);
         lds = stack_bytes(s);
     }
-FrameLaunch L{mode, md, tex, use_lds, grid, block, lds, st};
+    FrameLaunch L{mode, md, tex, use_lds, grid, block, lds, st};
     if (s->ext) kext::launch_frame(s->view, F, L);
     else kcore::launch_frame(s->view, F, L);
     HIP_TRY(hipGetLastError());

@@ -27,6 +27,10 @@ for s in "$@"; do
             step pmc_valu 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_valu -o pmc -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
             step pmc_sum 60 python tools/pmc_summary.py teapotF_1920x1080_spp1_d1 gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_latest.json ;;
         listpmc) step listpmc 120 rocprofv3 -L ;;
+        pmclds)
+            step pmc_lds 600 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT --output-format csv -d gpurun_out/pmc_lds -o pmc -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+        pmcact)
+            step pmc_act 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS --output-format csv -d gpurun_out/pmc_act -o pmc -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
         pmcmem)
             step pmc_mem1 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/pmc_mem1 -o pmc -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline
             step pmc_mem2 600 rocprofv3 --pmc TA_BUSY_avr TA_BUSY_max TCP_TOTAL_CACHE_ACCESSES_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d gpurun_out/pmc_mem2 -o pmc -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;

@@ -23,6 +23,8 @@ struct DevMaterial {
 struct SceneView {
     const float4 *__restrict__ nodes;   // 2 float4 per node
     const float4 *__restrict__ pairs;   // 4 float4 per child pair (X, Y, Z, words), pair k at 4k
+    const float4 *__restrict__ pairs48; // 3 float4 per child pair (X, Y, Z), pair k at 3k
+    const uint32_t *__restrict__ words; // node words (leftFirst << 8 | count) by node index
     const float4 *__restrict__ prims;   // 3 float4 per leaf slot
     const float4 *__restrict__ shade;   // 2 float4 per primitive id
     const DevMaterial *__restrict__ mats;
@@ -43,6 +45,7 @@ struct SceneView {
     int bounds_finite;                  // every node bound is a finite float
     uint32_t stack_entries;             // LDS stack entries per lane
     uint32_t node_f4;                   // node array size in float4s
+    uint32_t p48_f4, words_n;           // pairs48 size in float4s, words count
     int wave_primary;                   // camera rays take the wave-coherent walk
 };
 
@@ -63,7 +66,7 @@ struct FrameLaunch {
     int mode;        // RT_MODE_*
     int md;          // depth bucket: 1, 4, 10 or 32
     bool tex;        // non-constant sky texture
-    bool lds;        // k_render_lds (primary+shadow, nodes in LDS)
+    int lds;         // 0 global nodes; 64: k_render_lds (1024 threads); 48: k_render_lds48 (512)
     dim3 grid, block;
     size_t lds_bytes;
     hipStream_t stream;

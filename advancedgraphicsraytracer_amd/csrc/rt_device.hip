@@ -33,6 +33,10 @@
 #include "rt_dev_types.h"
 #include "rt_internal.h"
 
+#ifndef RT_LDS_WG_TILES
+#define RT_LDS_WG_TILES 16   // must match rt_kernels.inc
+#endif
+
 
 // ====================================================================== host side
 using namespace rt;
@@ -52,12 +56,12 @@ struct rt_scene {
     Bvh bvh;
     uint32_t num_prims = 0;
     uint32_t stack_depth = 0;   // LDS stack entries per lane
-    bool lds_nodes = false;     // frame kernel keeps the node array in LDS (k_render_lds)
+    int lds_kernel = 0;         // primary+shadow frames: 64 = k_render_lds, 48 = k_render_lds48, 0 = global nodes
     uint32_t num_cus = 256;     // persistent grid size of k_render_lds
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
     bool ext = false;           // needs the kext kernels (cubes, quads, textures, non-Light light)
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
-    void *d_xprims = nullptr, *d_tex = nullptr, *d_pairs = nullptr;
+    void *d_xprims = nullptr, *d_tex = nullptr, *d_pairs = nullptr, *d_pairs48 = nullptr, *d_words = nullptr;
     void *d_scratch = nullptr;  // staging for the host-pointer batched calls
     size_t scratch_bytes = 0;
     hipStream_t stream = nullptr;
@@ -127,7 +131,7 @@ void free_scene(rt_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     (void)hipDeviceSynchronize();
-    void *ptrs[] = {s->d_nodes, s->d_pairs, s->d_prims, s->d_shade, s->d_mats, s->d_sky, s->d_xprims, s->d_tex,
+    void *ptrs[] = {s->d_nodes, s->d_pairs, s->d_pairs48, s->d_words, s->d_prims, s->d_shade, s->d_mats, s->d_sky, s->d_xprims, s->d_tex,
                     s->d_scratch};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -155,6 +159,8 @@ inline f3 tvec_host(float4 r0, float4 r1, float4 r2, f3 a) {
     const float M[12] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w};
     return tvec(M, a);
 }
+
+size_t lds48_scene_bytes(const rt_scene *s);
 
 int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (!d || !out || !d->prims || d->num_prims == 0 || !d->materials || d->num_materials == 0)
@@ -249,6 +255,12 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         pairs[4 * k + 2] = make_float4(a.mn[2], b.mn[2], a.mx[2], b.mx[2]);
         pairs[4 * k + 3] = make_float4(ubits(wa), ubits(wb), 0.0f, 0.0f);
     }
+    // ... and as 48-B pairs (X, Y, Z) plus one word per node for k_render_lds48
+    std::vector<float4> pairs48(3 * (size_t)(s->bvh.nodes_used / 2 + 1), make_float4(0, 0, 0, 0));
+    std::vector<uint32_t> words(s->bvh.nodes_used, 0u);
+    for (uint32_t k = 1; 2 * k + 1 < s->bvh.nodes_used; ++k)
+        for (int c = 0; c < 3; ++c) pairs48[3 * k + c] = pairs[4 * k + c];
+    for (uint32_t i = 0; i < s->bvh.nodes_used; ++i) words[i] = (s->bvh.nodes[i].leftFirst << 8) | s->bvh.nodes[i].count;
     // ---- leaf-order primitive records and per-id shading records; cubes and quads keep
     // their matrices and data in a side table (8 float4 each)
     static const float I16[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
@@ -372,6 +384,8 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     rc = RT_OK;
     if (rc == RT_OK) rc = upload(&s->d_nodes, nodes);
     if (rc == RT_OK) rc = upload(&s->d_pairs, pairs);
+    if (rc == RT_OK) rc = upload(&s->d_pairs48, pairs48);
+    if (rc == RT_OK) rc = upload(&s->d_words, words);
     if (rc == RT_OK) rc = upload(&s->d_prims, prims);
     if (rc == RT_OK) rc = upload(&s->d_shade, shade);
     if (rc == RT_OK) rc = upload(&s->d_mats, mats);
@@ -385,6 +399,10 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     SceneView &v = s->view;
     v.nodes = (const float4 *)s->d_nodes;
     v.pairs = (const float4 *)s->d_pairs;
+    v.pairs48 = (const float4 *)s->d_pairs48;
+    v.words = (const uint32_t *)s->d_words;
+    v.p48_f4 = (uint32_t)pairs48.size();
+    v.words_n = (uint32_t)words.size();
     v.prims = (const float4 *)s->d_prims;
     v.shade = (const float4 *)s->d_shade;
     v.mats = (const DevMaterial *)s->d_mats;
@@ -427,9 +445,18 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     }
     v.stack_entries = s->stack_depth;
     v.node_f4 = 2u * s->bvh.nodes_used;
-#ifndef RT_DISABLE_LDS_SCENE
-    s->lds_nodes = (size_t)s->stack_depth * 4096u + (size_t)s->bvh.nodes_used * 32u <= 160u * 1024u;
-#endif
+    // LDS kernels, preferred in this order: two 512-thread workgroups per CU (k_render_lds48)
+    // when half the LDS holds the 48-B pairs, words and u16 stacks; one 1024-thread group
+    // (k_render_lds) when the 64-B pairs and u32 stacks fit; else global nodes.
+    // RT_LDS_KERNEL=48/64/0 overrides (A/B runs).
+    if (lds48_scene_bytes(s) <= 80u * 1024u) s->lds_kernel = 48;
+    else if ((size_t)s->stack_depth * 4096u + (size_t)s->bvh.nodes_used * 32u <= 160u * 1024u) s->lds_kernel = 64;
+    if (const char *e = std::getenv("RT_LDS_KERNEL")) {
+        const int k = std::atoi(e);
+        if (k == 0 || (k == 64 && (size_t)s->stack_depth * 4096u + (size_t)s->bvh.nodes_used * 32u <= 160u * 1024u) ||
+            (k == 48 && lds48_scene_bytes(s) <= 160u * 1024u))
+            s->lds_kernel = k;
+    }
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
     v.wave_primary = 0;
     if (const char *e = std::getenv("RT_WAVE_PRIMARY")) v.wave_primary = std::atoi(e) != 0 && !s->has_cubes;
@@ -446,6 +473,10 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 
 size_t stack_bytes(const rt_scene *s) { return (size_t)s->stack_depth * 256u * sizeof(uint32_t); }
 // k_render_lds: [stack_entries][1024] u32 stacks, then the node array
+// k_render_lds48: [stack_entries][512] u16 stacks, 48-B pairs, node words
+size_t lds48_scene_bytes(const rt_scene *s) {
+    return (size_t)s->stack_depth * 512u * 2u + (size_t)s->view.p48_f4 * 16u + (size_t)s->view.words_n * 4u;
+}
 size_t lds_scene_bytes(const rt_scene *s) {
     return (size_t)s->stack_depth * 1024u * sizeof(uint32_t) + (size_t)s->bvh.nodes_used * 32u;
 }
@@ -486,19 +517,23 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     // LDS nodes pay off where registers allow 1024-thread workgroups without spilling:
     // the primary+shadow kernel with the constant sky (103 VGPRs); the path-tracing
     // variants keep the 256-thread global-node kernel (A/B in profiles/r01).
-    const bool use_lds = s->lds_nodes && mode == RT_MODE_PATH && md == 1 && !tex;
+    const int lds_kind = (mode == RT_MODE_PATH && md == 1 && !tex) ? s->lds_kernel : 0;
     dim3 grid, block;
     size_t lds;
-    if (use_lds) {
-        grid = dim3((F.ntiles_local + 15) / 16);
+    if (lds_kind == 64) {
+        grid = dim3((F.ntiles_local + RT_LDS_WG_TILES - 1) / RT_LDS_WG_TILES);
         block = dim3(1024);
         lds = lds_scene_bytes(s);
+    } else if (lds_kind == 48) {
+        grid = dim3((F.ntiles_local + 7) / 8);
+        block = dim3(512);
+        lds = lds48_scene_bytes(s);
     } else {
         grid = dim3((F.ntiles_local + 3) / 4);
         block = dim3(256);
         lds = stack_bytes(s);
     }
-    FrameLaunch L{mode, md, tex, use_lds, grid, block, lds, st};
+    FrameLaunch L{mode, md, tex, lds_kind, grid, block, lds, st};
     if (s->ext) kext::launch_frame(s->view, F, L);
     else kcore::launch_frame(s->view, F, L);
     HIP_TRY(hipGetLastError());

@@ -86,12 +86,18 @@ def main():
     if world != args.gpus:
         args.gpus = world if world > 1 else args.gpus
     dist = None
+    # one rank per GPU; RT_DIST_BACKEND=gloo + fewer GPUs than ranks rehearses the N > 1 path
+    # on a single card (ranks share it; the exchange goes through gloo instead of RCCL)
+    device = local % max(1, torch.cuda.device_count()) if world > 1 else 0
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = local if world > 1 else 0
+        torch.cuda.set_device(device)
+        backend = os.environ.get("RT_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(device)
 
     W, H = args.width, args.height

@@ -47,13 +47,11 @@ def main():
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--check", action="store_true")
     a = ap.parse_args()
-    builds = []
-    cfg = {}
+    builds = []      # (key, spec, lib, scene, renderer, camera, out, mode, depth) per entry
     loaded = {}
-    for p in a.libs:
+    for i, p in enumerate(a.libs):
         path, _, opts = p.partition("@")
         kv = dict(o.split("=") for o in opts.split(",") if o)
-        cfg[p] = (int(kv.get("mode", 0)), int(kv.get("depth", a.depth)))
         L = loaded.get(path) or load(path)
         loaded[path] = L
         for k, v in kv.items():              # upper-case options are environment knobs read at scene creation
@@ -67,17 +65,19 @@ def main():
         cam = rt.Camera()
         L.rt_camera_default(a.w, a.h, C.byref(cam))
         out = torch.zeros(a.w * a.h, dtype=torch.int32, device="cuda")
-        builds.append((p, L, sc, r, cam, out))
+        key = os.path.basename(p)
+        if key in [bd[0] for bd in builds]:   # the same entry listed twice (position-bias checks)
+            key = f"{key}#{i}"
+        builds.append((key, p, L, sc, r, cam, out, int(kv.get("mode", 0)), int(kv.get("depth", a.depth))))
         for k in kv:
             if k.isupper():
                 del os.environ[k]
-    times = {p: [] for p in a.libs}
+    times = [[] for _ in builds]
     frame = 0
     for rnd in range(a.rounds):
-        for p, L, sc, r, cam, out in builds:
+        for i, (key, p, L, sc, r, cam, out, mode, depth) in enumerate(builds):
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             # warm + timed frames on the default stream
-            mode, depth = cfg[p]
             fp = rt.FrameParams(a.w, a.h, a.spp, depth, frame, mode, 0)
             L.rt_render_frame(r, C.byref(cam), C.byref(fp), C.c_void_p(out.data_ptr()), None)
             ev[0].record()
@@ -87,26 +87,26 @@ def main():
                 assert rc == 0, L.rt_last_error()
             ev[1].record()
             torch.cuda.synchronize()
-            times[p].append(ev[0].elapsed_time(ev[1]) / a.frames)
+            times[i].append(ev[0].elapsed_time(ev[1]) / a.frames)
         frame += a.frames + 1
     res = {}
-    for p, L, sc, r, cam, out in builds:
+    for i, (key, p, L, sc, r, cam, out, mode, depth) in enumerate(builds):
         c = rt.Counters()
         L.rt_renderer_counters(r, C.byref(c))
-        t = np.array(times[p])
+        t = np.array(times[i])
         rays_per_frame = (c.primary + c.shadow + c.bounce) / max(1, c.frames)
-        res[os.path.basename(p)] = {"mode": cfg[p][0], "depth": cfg[p][1],"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(t.min()), 4),
-                                    "mrays_s": round(rays_per_frame / (np.median(t) * 1e-3) / 1e6, 1)}
+        res[key] = {"mode": mode, "depth": depth, "median_ms": round(float(np.median(t)), 4),
+                    "min_ms": round(float(t.min()), 4), "mrays_s": round(rays_per_frame / (np.median(t) * 1e-3) / 1e6, 1)}
     if a.check:
         ref = None
-        for p, L, sc, r, cam, out in builds:
-            fr = rt.FrameParams(a.w, a.h, a.spp, cfg[p][1], 12345, cfg[p][0], 1)
+        for key, p, L, sc, r, cam, out, mode, depth in builds:
+            fr = rt.FrameParams(a.w, a.h, a.spp, depth, 12345, mode, 1)
             L.rt_render_frame(r, C.byref(cam), C.byref(fr), C.c_void_p(out.data_ptr()), None)
             torch.cuda.synchronize()
             img = out.cpu().numpy().copy()
             if ref is None:
                 ref = img
-            res[os.path.basename(p)]["same_image_as_first"] = bool(np.array_equal(img, ref))
+            res[key]["same_image_as_first"] = bool(np.array_equal(img, ref))
     print(json.dumps({"scene": a.scene, "w": a.w, "h": a.h, "spp": a.spp, "depth": a.depth, "results": res}, indent=1))
 
 

@@ -28,7 +28,7 @@ DIFFUSE, MIRROR, DIELECTRIC, CHECKERBOARD, LIGHT, DSMIX, TEXTURE = 0, 1, 2, 3, 4
 MODE_PATH = 0
 MODE_WHITTED = 1
 MODE_PACKET = 2
-WALK_LANE, WALK_WAVE = 0, 1
+WALK_LANE, WALK_WAVE, WALK_AUTO = 0, 1, 2
 # renderer.h:9, renderer.h:13, renderer.cpp:105 (TracePacket's bounces: Trace's default depth)
 DEFAULT_DEPTH = {MODE_PATH: 10, MODE_WHITTED: 20, MODE_PACKET: 10}
 RECIPES = ("teapotF", "teapot", "mig16", "cfg3", "cfg5")
@@ -438,7 +438,7 @@ class Scene:
         return hits[:, 0], hits.view(torch.int32)[:, 1], hits[:, 2], hits[:, 3]
 
     def set_camera_walk(self, walk):
-        """WALK_LANE (default) or WALK_WAVE: how camera rays walk the BVH (same results)."""
+        """WALK_LANE, WALK_WAVE or WALK_AUTO (default): how camera rays walk the BVH (same results)."""
         _check(self.L.rt_scene_set_camera_walk(self.h, walk))
 
     def IntersectBVHPacket(self, rays, stream=None):

@@ -59,6 +59,7 @@ struct rt_scene {
     int lds_kernel = 0;         // primary+shadow frames: 64 = k_render_lds, 48 = k_render_lds48, 0 = global nodes
     uint32_t num_cus = 256;     // persistent grid size of k_render_lds
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
+    int walk = RT_WALK_LANE;    // camera-ray walk of the global-node primary+shadow kernel
     bool ext = false;           // needs the kext kernels (cubes, quads, textures, non-Light light)
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
     void *d_xprims = nullptr, *d_tex = nullptr, *d_pairs = nullptr, *d_pairs48 = nullptr, *d_words = nullptr;
@@ -75,6 +76,11 @@ struct rt_renderer {
     uint32_t *d_rgb = nullptr;   // staging frame for rt_render_frame_host
     uint64_t primary = 0, frames = 0;
     hipStream_t stream = nullptr;
+    // RT_WALK_AUTO: the first eligible frames time the lane walk and the wave walk on the
+    // caller's stream (one warm-up, one each), the fourth picks the faster for good
+    int tune = 0;
+    bool wave = false;
+    hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -459,7 +465,8 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     }
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
     v.wave_primary = 0;
-    if (const char *e = std::getenv("RT_WAVE_PRIMARY")) v.wave_primary = std::atoi(e) != 0 && !s->has_cubes;
+    s->walk = s->has_cubes ? RT_WALK_LANE : RT_WALK_AUTO;
+    if (const char *e = std::getenv("RT_WAVE_PRIMARY")) s->walk = std::atoi(e) != 0 && !s->has_cubes ? RT_WALK_WAVE : RT_WALK_LANE;
     v.bounds_finite = 1;
     for (uint32_t i = 0; i < s->bvh.nodes_used && v.bounds_finite; ++i) {
         if (i == 1) continue;
@@ -534,9 +541,35 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         lds = stack_bytes(s);
     }
     FrameLaunch L{mode, md, tex, lds_kind, grid, block, lds, st};
-    if (s->ext) kext::launch_frame(s->view, F, L);
-    else kcore::launch_frame(s->view, F, L);
+    SceneView view = s->view;
+    // camera-ray walk (only the global-node primary+shadow kernel has both)
+    const bool walk_kernel = mode == RT_MODE_PATH && md == 1 && lds_kind == 0 && !s->ext;
+    int timed = -1;   // tev pair recorded around this launch
+    if (walk_kernel) {
+        if (s->walk == RT_WALK_WAVE) view.wave_primary = 1;
+        else if (s->walk == RT_WALK_AUTO) {
+            if (r->tune < 3) {
+                if (!r->tev[0])
+                    for (auto &e : r->tev) HIP_TRY(hipEventCreate(&e));
+                if (r->tune == 1) timed = 0;                       // lane walk
+                if (r->tune == 2) { timed = 2; view.wave_primary = 1; }
+                ++r->tune;
+            } else if (r->tune == 3) {                             // decide once, after both timed frames
+                float tl = 0, tw = 0;
+                HIP_TRY(hipEventSynchronize(r->tev[3]));
+                HIP_TRY(hipEventElapsedTime(&tl, r->tev[0], r->tev[1]));
+                HIP_TRY(hipEventElapsedTime(&tw, r->tev[2], r->tev[3]));
+                r->wave = tw < tl;
+                r->tune = 4;
+            }
+            if (r->tune == 4) view.wave_primary = r->wave ? 1 : 0;
+        }
+    }
+    if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed], st));
+    if (s->ext) kext::launch_frame(view, F, L);
+    else kcore::launch_frame(view, F, L);
     HIP_TRY(hipGetLastError());
+    if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed + 1], st));
     // pixels covered by this launch (primary rays per sample)
     uint64_t px = (uint64_t)F.ntiles_local * 64u;
     if ((r->W & 7u) || (r->H & 7u)) {
@@ -608,10 +641,11 @@ int rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
 
 int rt_scene_set_camera_walk(rt_scene *s, int walk) {
     if (!s) return fail(RT_ERR_INVALID, "null argument");
-    if (walk != RT_WALK_LANE && walk != RT_WALK_WAVE) return fail(RT_ERR_INVALID, "unknown camera walk");
-    if (walk == RT_WALK_WAVE && s->has_cubes)
+    if (walk != RT_WALK_LANE && walk != RT_WALK_WAVE && walk != RT_WALK_AUTO)
+        return fail(RT_ERR_INVALID, "unknown camera walk");
+    if (walk != RT_WALK_LANE && s->has_cubes)
         return fail(RT_ERR_UNSUPPORTED, "the wave walk needs order-independent hits; cubes accept on tmax (Primitive.h:221-233)");
-    s->view.wave_primary = walk == RT_WALK_WAVE;
+    s->walk = walk;
     return RT_OK;
 }
 
@@ -720,6 +754,8 @@ int rt_renderer_destroy(rt_renderer *r) {
     (void)hipFree(r->d_acc);
     (void)hipFree(r->d_counters);
     if (r->d_rgb) (void)hipFree(r->d_rgb);
+    for (auto &e : r->tev)
+        if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(r->stream);
     delete r;
     return RT_OK;

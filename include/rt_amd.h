@@ -160,14 +160,17 @@ int rt_scene_create_recipe(const char *name, const char *mesh_dir, int32_t devic
 int rt_scene_destroy(rt_scene *s);
 int rt_scene_get_info(const rt_scene *s, rt_scene_info *info);
 /* How the primary+shadow frame kernel walks the BVH for camera rays (results identical):
- * RT_WALK_LANE (default) -- one traversal per lane, the reference's order;
+ * RT_WALK_LANE -- one traversal per lane, the reference's order;
  * RT_WALK_WAVE -- the wave's 64 rays (an 8x8 tile) walk the union of their subtrees with
  *   a wave-uniform node and stack; lanes whose closest hit could depend on the visiting
  *   order (an exact distance tie, or a hit nearer than its leaf box's entry) are re-traced
  *   in the reference order.  Faster where rays share most of their walk (mig29 x16: 1.9x);
- *   slower where they split early (CFG3-sub).  Only used by scenes whose nodes are not
- *   held in LDS.  The environment variable RT_WAVE_PRIMARY=0/1 sets it at creation. */
-enum { RT_WALK_LANE = 0, RT_WALK_WAVE = 1 };
+ *   slower where they split early (CFG3-sub);
+ * RT_WALK_AUTO (default; LANE for scenes with cubes) -- each renderer times one frame of
+ *   each after a warm-up frame and keeps the faster.
+ * Only scenes whose nodes are not held in LDS use it.  RT_WAVE_PRIMARY=0/1 in the
+ * environment forces LANE / WAVE at scene creation. */
+enum { RT_WALK_LANE = 0, RT_WALK_WAVE = 1, RT_WALK_AUTO = 2 };
 int rt_scene_set_camera_walk(rt_scene *s, int walk);
 /* host copy of the BVH in use (nodes_used x 32 B, num_prims x u32) */
 int rt_scene_copy_bvh(const rt_scene *s, void *nodes, uint32_t *indices);

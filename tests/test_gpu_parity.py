@@ -382,11 +382,12 @@ def test_compat_host_program_on_gpu(rt, torch, tmp_path):
 
 # ---- wave-coherent camera-ray walk (rt_scene_set_camera_walk): same frames, same counts
 @pytest.mark.parametrize("name,W,H", [("mig16", 480, 270), ("cfg3", 320, 180), ("cfg5", 333, 201)])
-def test_wave_camera_walk_bit_exact(rt, oracle, torch, name, W, H):
+@pytest.mark.parametrize("walk", ["WALK_WAVE", "WALK_AUTO"])
+def test_wave_camera_walk_bit_exact(rt, oracle, torch, name, W, H, walk):
     g = rt.Scene.recipe(name)
-    g.set_camera_walk(rt.WALK_WAVE)
+    g.set_camera_walk(getattr(rt, walk))
     o = oracle.Scene(name, rt.DATA_DIR)
-    got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, W, H, 1, 1, frames=2)
+    got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, W, H, 1, 1, frames=5)   # AUTO: warm, lane, wave, pick
     assert np.array_equal(got, want)
     assert np.array_equal(gacc.view(np.uint32), acc.view(np.uint32))
     assert c["shadow"] == st["shadow"]

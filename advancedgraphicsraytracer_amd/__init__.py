@@ -143,6 +143,7 @@ def lib():
         "rt_renderer_counters": ([vp, C.POINTER(Counters)], C.c_int),
         "rt_renderer_read_accumulator": ([vp, fp], C.c_int),
         "rt_renderer_stream": ([vp, C.POINTER(vp)], C.c_int),
+        "rt_frame_kernel_name": ([vp, C.POINTER(FrameParams)], C.c_char_p),
         "rt_synchronize": ([vp], C.c_int),
     }
     for name, (args, res) in sigs.items():
@@ -565,6 +566,13 @@ class Renderer:
         _check(self.L.rt_assemble_shards(self.h, C.c_void_p(gathered.data_ptr()), num_shards,
                                          C.c_void_p(out.data_ptr()), C.c_void_p(s)))
         return out
+
+    def kernel_name(self, spp=1, depth=None):
+        """The frame kernel Tick launches for these params (rocprofv3 name, abbreviated)."""
+        name = self.L.rt_frame_kernel_name(self.h, C.byref(self.params(spp, depth)))
+        if name is None:
+            raise RTError(-1, self.L.rt_last_error().decode())
+        return name.decode()
 
     def counters(self):
         c = Counters()

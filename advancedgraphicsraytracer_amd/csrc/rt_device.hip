@@ -488,6 +488,15 @@ size_t lds_scene_bytes(const rt_scene *s) {
     return (size_t)s->stack_depth * 1024u * sizeof(uint32_t) + (size_t)s->bvh.nodes_used * 32u;
 }
 
+// the compiled MAXD class a Trace depth runs in
+int max_depth_class(uint32_t depth) { return depth <= 1 ? 1 : depth <= 4 ? 4 : depth <= 10 ? 10 : 32; }
+// LDS nodes pay off where registers allow 1024/512-thread workgroups without spilling:
+// the primary+shadow kernel with the constant sky; the path-tracing variants keep the
+// 256-thread global-node kernel (A/B in profiles/r01).
+int lds_kind_for(const rt_scene *s, int mode, int md) {
+    return (mode == RT_MODE_PATH && md == 1 && s->view.sky_const) ? s->lds_kernel : 0;
+}
+
 int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
                   uint32_t *out, int packed, void *stream) {
     if (!r || !cam || !p || !out) return fail(RT_ERR_INVALID, "rt_render: null argument");
@@ -518,13 +527,10 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     hipStream_t st = (hipStream_t)stream;
     const uint32_t depth = p->depth;
     if (depth > 32) return fail(RT_ERR_UNSUPPORTED, "Trace depth above 32");   // = kWHITTED_MAX
-    const int md = depth <= 1 ? 1 : depth <= 4 ? 4 : depth <= 10 ? 10 : 32;
+    const int md = max_depth_class(depth);
     const bool tex = !s->view.sky_const;
     const int mode = (int)p->mode;
-    // LDS nodes pay off where registers allow 1024-thread workgroups without spilling:
-    // the primary+shadow kernel with the constant sky (103 VGPRs); the path-tracing
-    // variants keep the 256-thread global-node kernel (A/B in profiles/r01).
-    const int lds_kind = (mode == RT_MODE_PATH && md == 1 && !tex) ? s->lds_kernel : 0;
+    const int lds_kind = lds_kind_for(s, mode, md);
     dim3 grid, block;
     size_t lds;
     if (lds_kind == 64) {
@@ -819,6 +825,24 @@ int rt_renderer_read_accumulator(rt_renderer *r, float *host) {
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(host, r->d_acc, sizeof(float4) * (size_t)r->W * r->H, hipMemcpyDeviceToHost));
     return RT_OK;
+}
+
+const char *rt_frame_kernel_name(const rt_renderer *r, const rt_frame_params *p) {
+    if (!r || !p || p->mode > RT_MODE_PACKET || p->depth > 32) {
+        fail(RT_ERR_INVALID, "rt_frame_kernel_name: bad argument");
+        return nullptr;
+    }
+    const rt_scene *s = r->scene;
+    const int md = max_depth_class(p->depth);
+    const int lds_kind = lds_kind_for(s, (int)p->mode, md);
+    if (lds_kind == 48) return "k_render_lds48<1>";
+    if (lds_kind == 64) return "k_render_lds<1>";
+    static const char *names[3][4] = {
+        {"k_render<path,1>", "k_render<path,4>", "k_render<path,10>", "k_render<path,32>"},
+        {"k_render<whitted,1>", "k_render<whitted,1>", "k_render<whitted,1>", "k_render<whitted,1>"},
+        {"k_render<packet,1>", "k_render<packet,10>", "k_render<packet,10>", "k_render<packet,32>"}};
+    const int col = md == 1 ? 0 : md == 4 ? 1 : md == 10 ? 2 : 3;
+    return names[p->mode][col];
 }
 
 int rt_renderer_stream(rt_renderer *r, void **stream) {

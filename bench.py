@@ -10,7 +10,9 @@ timing; synthetic data = the bundled teapot mesh + the synthetic constant sky.
 N > 1 (python -m torch.distributed.run ... bench.py --gpus N): weak scaling -- the
 frame's 8x8 tiles are interleaved over the ranks and the frame is rendered at spp = N,
 so every GPU traces one 1080p frame's worth of samples per step; one RCCL all-gather of
-the packed RGB8 tiles per frame assembles the image on rank 0.
+the packed RGB8 tiles per frame assembles the image on rank 0.  The
+gather of frame i runs while frame i+1 renders (double-buffered tiles); the timed region
+ends after the last frame's gather and assembly.
 value = all rays traced by all ranks / max-over-ranks wall time.
 """
 import argparse
@@ -114,19 +116,25 @@ def main():
 
     def step(i, events=None):
         with torch.cuda.stream(stream):
+            if sharded is not None:
+                # the one collective per frame: frame i's packed tiles are gathered while
+                # frame i+1 renders; rank 0 assembles frame i once its gather is done
+                sharded.submit(spp=spp, depth=args.depth, frame=i, stream=sptr, events=events)
+                return
             if events is not None:
                 events[0].record(stream)
-            if sharded is not None:
-                sharded.render_local(spp=spp, depth=args.depth, frame=i, stream=sptr)
-            else:
-                rend.Tick(frame_out, spp=spp, depth=args.depth, frame=i, stream=sptr)
+            rend.Tick(frame_out, spp=spp, depth=args.depth, frame=i, stream=sptr)
             if events is not None:
                 events[1].record(stream)
-            if sharded is not None:   # the one collective per frame: gather packed tiles, rank 0 assembles
-                sharded.exchange(stream=sptr)
+
+    def drain():
+        if sharded is not None:
+            with torch.cuda.stream(stream):
+                sharded.flush(stream=sptr)
 
     for i in range(args.warmup):
         step(i)
+    drain()
     torch.cuda.synchronize(device)
     c0 = rend.counters()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -136,6 +144,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k, evs[k])
+    drain()                                 # the last frame's gather + assembly are inside the timed region
     torch.cuda.synchronize(device)
     if dist:
         dist.barrier()
@@ -171,7 +180,7 @@ def main():
                 traffic = None
             roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                        "kernel": "k_render<1>", "kernel_ms": round(kern_ms, 4),
+                        "kernel": rend.kernel_name(spp=spp, depth=args.depth), "kernel_ms": round(kern_ms, 4),
                         "bytes_per_ray": {"primary": round(bp, 1), "shadow": round(bs, 1)}}
         line = {
             "metric": "Mrays/s (primary+shadow) at 1080p",

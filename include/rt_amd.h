@@ -212,6 +212,10 @@ int rt_assemble_shards(rt_renderer *r, const uint32_t *gathered_dev, uint32_t nu
 int rt_renderer_counters(rt_renderer *r, rt_counters *out);
 /* accumulator readback, W*H float4 */
 int rt_renderer_read_accumulator(rt_renderer *r, float *host_out);
+/* Name of the frame kernel rt_render_frame / rt_render_shard launch for these params
+ * (as it appears in rocprofv3 kernel traces, template arguments abbreviated); for
+ * profiling and the bench's roofline line.  NULL on a bad argument. */
+const char *rt_frame_kernel_name(const rt_renderer *r, const rt_frame_params *p);
 int rt_renderer_stream(rt_renderer *r, void **stream);
 int rt_synchronize(rt_renderer *r);
 

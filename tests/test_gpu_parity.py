@@ -446,3 +446,15 @@ def test_quad_light(rt, oracle, torch, mode, depth):
     got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, 120, 80, 1, depth, mode=mode)
     assert np.abs(gacc - acc).max() <= PIX_TOL
     assert c["shadow"] == st["shadow"]
+
+
+@pytest.mark.gpu
+def test_frame_kernel_name(rt):
+    """rt_frame_kernel_name names the kernel the bench's roofline line is about."""
+    s = rt.Scene.recipe("teapotF")
+    r = rt.Renderer(s, 64, 64)
+    assert r.kernel_name(spp=1, depth=1) == "k_render_lds48<1>"
+    assert r.kernel_name(spp=1, depth=10) == "k_render<path,10>"
+    r.mode = rt.MODE_WHITTED
+    assert r.kernel_name(spp=1, depth=5) == "k_render<whitted,1>"
+    r.close()

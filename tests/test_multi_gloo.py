@@ -66,6 +66,17 @@ def worker(rank, world, port, q):
             img = sf.render(spp=1, depth=1, frame=frame)
             if rank == 0:
                 ok &= bool(np.array_equal(img.numpy(), r.full_frame(frame)))
+        # pipelined: submit(i) completes frame i-1, flush() the last one
+        done = []
+        for frame in (2, 3, 4):
+            img = sf.submit(spp=1, depth=1, frame=frame)
+            if img is not None:
+                done.append(img.numpy().copy())
+        img = sf.flush()
+        if rank == 0:
+            done.append(img.numpy().copy())
+            ok &= len(done) == 3
+            ok &= all(np.array_equal(d, r.full_frame(f)) for d, f in zip(done, (2, 3, 4)))
         if rank == 0:
             q.put(ok)
     finally:

@@ -39,10 +39,20 @@ def worker(rank, world, port, q):
             torch.cuda.synchronize()
             if rank == 0:
                 frames.append(out.cpu().numpy().copy())
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):   # pipelined: frame f's gather overlaps frame f+1's render
+            for f in range(2, 4):
+                out = sf.submit(spp=2, depth=3, frame=f, stream=st.cuda_stream)
+                if out is not None:
+                    torch.cuda.synchronize()
+                    frames.append(out.cpu().numpy().copy())
+            out = sf.flush(stream=st.cuda_stream)
+        torch.cuda.synchronize()
         if rank == 0:
+            frames.append(out.cpu().numpy().copy())
             ref = rt.Renderer(scene, W, H)
-            want = [ref.tick_host(spp=2, depth=3, frame=f).view(np.int32) for f in range(2)]
-            q.put(all(np.array_equal(a, b) for a, b in zip(frames, want)))
+            want = [ref.tick_host(spp=2, depth=3, frame=f).view(np.int32) for f in range(4)]
+            q.put(len(frames) == 4 and all(np.array_equal(a, b) for a, b in zip(frames, want)))
     except Exception as e:   # report, never hang the parent
         q.put(repr(e))
         raise

@@ -72,6 +72,30 @@ struct FrameLaunch {
     hipStream_t stream;
 };
 
+// Wavefront path tracing (RT_MODE_PATH, Trace depth >= 2): the frame's paths advance one
+// bounce per launch; between launches the paths still alive are compacted into a queue, so
+// every wave of a deep level works on 64 live paths instead of a handful.  Per path (index
+// p = (sample_in_batch * ntiles_local + local_tile) * 64 + lane):
+//   state  : 2 float4 -- (O.xyz, seed bits), (D.xyz, meta bits: d | levels << 8 |
+//            lastSpec << 16 | inside << 17)
+//   rec    : [level][p] 2 float4 -- the fold record of a bounce (BRDF or albedo, dot;
+//            Ld, diffuse flag), folded innermost-first when the path ends
+//   result : float4, the path's Trace value
+// queue_in / queue_out: path indices alive at this level / the next; qcount[level] their
+// counts (level 0 = every path of the batch, no queue).  sum: the per-pixel running sum
+// over the samples of earlier batches (sample order kept).
+struct PathArgs {
+    uint32_t s0, batch_spp, npaths, level;
+    uint32_t drain_level, drain_below;   // drain (run every remaining level) from this level on /
+                                         // at any level holding at most this many paths
+    float4 *state;
+    float4 *rec;
+    float4 *result;
+    uint32_t *queue_in, *queue_out;
+    uint32_t *qcount;
+    float4 *sum;
+};
+
 // Each kernel build provides the same launchers: `kcore` is compiled without the
 // extension primitives and materials (cubes, quads, quad light, TextureMaterial,
 // non-Light light materials), `kext` with them.  The host picks per scene.
@@ -84,6 +108,9 @@ struct FrameLaunch {
                          size_t lds, hipStream_t st);                                             \
     void launch_intersect_packet(const SceneView &S, const rt_ray *rays, rt_hit *hits,            \
                                  uint32_t n, hipStream_t st);                                     \
+    int launch_pt_level(const SceneView &S, const FrameArgs &F, const PathArgs &P, bool tex,      \
+                        bool full_grid, size_t lds, uint32_t num_cus, hipStream_t st);            \
+    void launch_pt_finish(const FrameArgs &F, const PathArgs &P, bool last, hipStream_t st);      \
     }
 RT_DECLARE_LAUNCHERS(kcore)
 RT_DECLARE_LAUNCHERS(kext)

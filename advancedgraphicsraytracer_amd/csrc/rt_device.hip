@@ -61,6 +61,12 @@ struct rt_scene {
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
     int walk = RT_WALK_LANE;    // camera-ray walk of the global-node primary+shadow kernel
     bool ext = false;           // needs the kext kernels (cubes, quads, textures, non-Light light)
+    bool pt_wavefront = true;   // depth >= 2 path tracing: wavefront (k_pt_level) vs one kernel (k_render)
+    uint32_t pt_drain_level = 64;   // bounce level from which the wavefront always drains (64 = never forced)
+    double pt_drain_rounds = 1.0;   // ... and it drains any level holding <= this many rounds of resident lanes
+    bool pt_full_grid = false;      // levels >= 1: one wave per queue slot group instead of a resident grid
+    uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per renderer: 12 GB of the 288 GB HBM
+                                              // holds all 16 spp of a 1080p depth-10 frame
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
     void *d_xprims = nullptr, *d_tex = nullptr, *d_pairs = nullptr, *d_pairs48 = nullptr, *d_words = nullptr;
     void *d_scratch = nullptr;  // staging for the host-pointer batched calls
@@ -81,6 +87,9 @@ struct rt_renderer {
     int tune = 0;
     bool wave = false;
     hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // wavefront path tracer (PathArgs): one allocation, grown on demand
+    void *d_pt = nullptr;
+    size_t pt_bytes = 0;
 };
 
 namespace {
@@ -463,6 +472,14 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
             (k == 48 && lds48_scene_bytes(s) <= 160u * 1024u))
             s->lds_kernel = k;
     }
+    // RT_PT_WAVEFRONT=0 selects the one-kernel path tracer (k_render<path, MAXD>) for A/B runs
+    if (const char *e = std::getenv("RT_PT_WAVEFRONT")) s->pt_wavefront = std::atoi(e) != 0;
+    // RT_PT_DRAIN_LEVEL / RT_PT_MEM_MB: wavefront drain level and path-state budget (A/B runs)
+    if (const char *e = std::getenv("RT_PT_DRAIN_LEVEL")) s->pt_drain_level = (uint32_t)std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("RT_PT_DRAIN_ROUNDS")) s->pt_drain_rounds = std::max(0.0, std::atof(e));
+    if (const char *e = std::getenv("RT_PT_FULL_GRID")) s->pt_full_grid = std::atoi(e) != 0;
+    if (const char *e = std::getenv("RT_PT_MEM_MB"))
+        s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
     v.wave_primary = 0;
     s->walk = s->has_cubes ? RT_WALK_LANE : RT_WALK_AUTO;
@@ -495,6 +512,78 @@ int max_depth_class(uint32_t depth) { return depth <= 1 ? 1 : depth <= 4 ? 4 : d
 // 256-thread global-node kernel (A/B in profiles/r01).
 int lds_kind_for(const rt_scene *s, int mode, int md) {
     return (mode == RT_MODE_PATH && md == 1 && s->view.sky_const) ? s->lds_kernel : 0;
+}
+
+// pixels covered by a frame / shard launch (primary rays per sample)
+uint64_t frame_pixels(const rt_renderer *r, const FrameArgs &F, uint32_t shard, uint32_t nshards, uint32_t tiles_x,
+                      uint32_t ntiles) {
+    uint64_t px = (uint64_t)F.ntiles_local * 64u;
+    if ((r->W & 7u) || (r->H & 7u)) {
+        px = 0;
+        for (uint32_t t = shard; t < ntiles; t += nshards) {
+            uint32_t tx = t % tiles_x, ty = t / tiles_x;
+            px += (uint64_t)std::min(8u, r->W - tx * 8) * std::min(8u, r->H - ty * 8);
+        }
+    }
+    return px;
+}
+
+
+// Wavefront path tracing of one frame / shard (PathArgs, rt_dev_types.h): the samples are
+// processed in batches that fit RT_PT_MEM_MB (default 12288 MB) of path state; per batch
+// one k_pt_level launch per bounce level, then k_pt_finish.
+int launch_pt_frame(rt_renderer *r, const FrameArgs &F, const SceneView &view, bool tex, hipStream_t st) {
+    rt_scene *s = r->scene;
+    const uint64_t npix = (uint64_t)F.ntiles_local * 64u;
+    const uint64_t per_path = 32u + 16u + 8u + (uint64_t)(F.depth - 1) * 32u;
+    const uint64_t budget = s->pt_mem_bytes;
+    uint64_t batch = std::max<uint64_t>(1, budget / (per_path * npix));
+    batch = std::min<uint64_t>(batch, F.spp);
+    if (batch * npix > 0xffffffffull / 2) batch = std::max<uint64_t>(1, (0xffffffffull / 2) / npix);
+    const uint64_t np = batch * npix;
+    const size_t need = (size_t)(np * per_path + npix * 16u + 64u * 4u + 4096u);
+    if (need > r->pt_bytes) {
+        if (r->d_pt) HIP_TRY(hipFree(r->d_pt));
+        r->d_pt = nullptr;
+        r->pt_bytes = 0;
+        HIP_TRY(hipMalloc(&r->d_pt, need));
+        r->pt_bytes = need;
+    }
+    char *b = static_cast<char *>(r->d_pt);
+    auto take = [&](size_t bytes) { char *q = b; b += (bytes + 255u) & ~(size_t)255u; return q; };
+    PathArgs P{};
+    P.state = reinterpret_cast<float4 *>(take(np * 32u));
+    P.result = reinterpret_cast<float4 *>(take(np * 16u));
+    uint32_t *q0 = reinterpret_cast<uint32_t *>(take(np * 4u));
+    uint32_t *q1 = reinterpret_cast<uint32_t *>(take(np * 4u));
+    P.sum = reinterpret_cast<float4 *>(take(npix * 16u));
+    P.qcount = reinterpret_cast<uint32_t *>(take(64u * 4u));
+    P.rec = reinterpret_cast<float4 *>(take((size_t)(F.depth - 1) * np * 32u));
+    const size_t lds = stack_bytes(s);
+    // levels are compacted level by level until one is small enough to drain (k_pt_level)
+    const uint32_t drain_level = s->pt_drain_level;
+    P.drain_level = drain_level;
+    P.drain_below = 0;
+    for (uint32_t s0 = 0; s0 < F.spp; s0 += (uint32_t)batch) {
+        P.s0 = s0;
+        P.batch_spp = std::min<uint32_t>((uint32_t)batch, F.spp - s0);
+        P.npaths = (uint32_t)(P.batch_spp * npix);
+        HIP_TRY(hipMemsetAsync(P.qcount, 0, 64u * 4u, st));
+        for (uint32_t level = 0; level < F.depth; ++level) {
+            P.level = level;
+            P.queue_in = (level & 1u) ? q1 : q0;
+            P.queue_out = (level & 1u) ? q0 : q1;
+            const int resident = s->ext ? kext::launch_pt_level(view, F, P, tex, s->pt_full_grid, lds, s->num_cus, st)
+                                        : kcore::launch_pt_level(view, F, P, tex, s->pt_full_grid, lds, s->num_cus, st);
+            if (level >= drain_level) break;           // that launch finished every remaining level
+            P.drain_below = (uint32_t)std::min<double>(4e9, s->pt_drain_rounds * resident);
+        }
+        const bool last = s0 + P.batch_spp >= F.spp;
+        if (s->ext) kext::launch_pt_finish(F, P, last, st);
+        else kcore::launch_pt_finish(F, P, last, st);
+    }
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
 }
 
 int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
@@ -546,6 +635,13 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         block = dim3(256);
         lds = stack_bytes(s);
     }
+    if (mode == RT_MODE_PATH && depth >= 2 && s->pt_wavefront) {
+        int rc = launch_pt_frame(r, F, s->view, tex, st);
+        if (rc != RT_OK) return rc;
+        r->primary += frame_pixels(r, F, shard, nshards, tiles_x, ntiles) * p->spp;
+        r->frames += 1;
+        return RT_OK;
+    }
     FrameLaunch L{mode, md, tex, lds_kind, grid, block, lds, st};
     SceneView view = s->view;
     // camera-ray walk (only the global-node primary+shadow kernel has both)
@@ -576,17 +672,8 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     else kcore::launch_frame(view, F, L);
     HIP_TRY(hipGetLastError());
     if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed + 1], st));
-    // pixels covered by this launch (primary rays per sample)
-    uint64_t px = (uint64_t)F.ntiles_local * 64u;
-    if ((r->W & 7u) || (r->H & 7u)) {
-        px = 0;
-        for (uint32_t t = shard; t < ntiles; t += nshards) {
-            uint32_t tx = t % tiles_x, ty = t / tiles_x;
-            px += (uint64_t)std::min(8u, r->W - tx * 8) * std::min(8u, r->H - ty * 8);
-        }
-    }
     (void)tiles_y;
-    r->primary += px * p->spp;
+    r->primary += frame_pixels(r, F, shard, nshards, tiles_x, ntiles) * p->spp;
     r->frames += 1;
     return RT_OK;
 }
@@ -760,6 +847,7 @@ int rt_renderer_destroy(rt_renderer *r) {
     (void)hipFree(r->d_acc);
     (void)hipFree(r->d_counters);
     if (r->d_rgb) (void)hipFree(r->d_rgb);
+    if (r->d_pt) (void)hipFree(r->d_pt);
     for (auto &e : r->tev)
         if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(r->stream);
@@ -833,6 +921,7 @@ const char *rt_frame_kernel_name(const rt_renderer *r, const rt_frame_params *p)
         return nullptr;
     }
     const rt_scene *s = r->scene;
+    if (p->mode == RT_MODE_PATH && p->depth >= 2 && s->pt_wavefront) return "k_pt_level";
     const int md = max_depth_class(p->depth);
     const int lds_kind = lds_kind_for(s, (int)p->mode, md);
     if (lds_kind == 48) return "k_render_lds48<1>";

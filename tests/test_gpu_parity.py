@@ -454,7 +454,37 @@ def test_frame_kernel_name(rt):
     s = rt.Scene.recipe("teapotF")
     r = rt.Renderer(s, 64, 64)
     assert r.kernel_name(spp=1, depth=1) == "k_render_lds48<1>"
-    assert r.kernel_name(spp=1, depth=10) == "k_render<path,10>"
+    assert r.kernel_name(spp=1, depth=10) == "k_pt_level"
     r.mode = rt.MODE_WHITTED
     assert r.kernel_name(spp=1, depth=5) == "k_render<whitted,1>"
     r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recipe,W,H,spp,depth,env", [
+    ("teapotF", 200, 120, 1, 10, {}),                           # one batch, adaptive drain
+    ("teapotF", 200, 120, 1, 10, {"RT_PT_DRAIN_ROUNDS": "0"}),  # compaction at every level
+    ("teapotF", 200, 120, 2, 10, {"RT_PT_DRAIN_LEVEL": "1"}),   # drain right after the camera rays
+    ("cfg3", 136, 80, 4, 4, {"RT_PT_MEM_MB": "1"}),             # 1 MB of path state: one sample per batch
+    ("cfg5", 96, 64, 3, 10, {"RT_PT_MEM_MB": "2"}),             # uneven batches
+    ("teapotF", 72, 40, 2, 2, {}),                              # depth 2: a single continuation level
+])
+def test_wavefront_equals_one_kernel_path_tracer(rt, torch, monkeypatch, recipe, W, H, spp, depth, env):
+    """The wavefront path tracer (k_pt_level + k_pt_finish: compaction between bounce
+    levels, drained deep levels, sample batches) must give the one-kernel path tracer's
+    frames bit for bit, accumulators included, over two frames; ray counters must agree."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("RT_PT_WAVEFRONT", "1")
+    s_wf = rt.Scene.recipe(recipe)
+    monkeypatch.setenv("RT_PT_WAVEFRONT", "0")
+    s_mk = rt.Scene.recipe(recipe)
+    r_wf, r_mk = rt.Renderer(s_wf, W, H), rt.Renderer(s_mk, W, H)
+    assert r_wf.kernel_name(spp=spp, depth=depth) == "k_pt_level"
+    assert r_mk.kernel_name(spp=spp, depth=depth).startswith("k_render<path")
+    for f in range(2):
+        a = r_wf.tick_host(spp=spp, depth=depth, frame=f)
+        b = r_mk.tick_host(spp=spp, depth=depth, frame=f)
+        assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
+    assert np.array_equal(r_wf.accumulator(), r_mk.accumulator())
+    assert r_wf.counters() == r_mk.counters()

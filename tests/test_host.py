@@ -29,9 +29,12 @@ def test_library_exports_every_header_symbol(rt):
         assert getattr(lib, n)
 
 
-def test_library_is_gfx950_code_object(rt):
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", rt.LIB_PATH],
-                         capture_output=True, text=True)
+def test_library_is_gfx950_code_object(rt, tmp_path):
+    # --offloading extracts the bundled code objects next to its input: run it on a copy
+    import shutil
+    lib = shutil.copy(rt.LIB_PATH, tmp_path / "librtamd.so")
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
+                         capture_output=True, text=True, cwd=tmp_path)
     text = out.stdout + out.stderr
     assert "gfx950" in text
 

@@ -68,8 +68,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--only", default="")
     ap.add_argument("--json", default="")
+    ap.add_argument("--custom", action="append", default=[], help="scene,w,h,spp,depth (repeatable)")
     a = ap.parse_args()
-    names = [n for n in CONFIGS if not a.only or any(o in n for o in a.only.split(","))]
+    for c in a.custom:
+        sc, w, h, spp, depth = c.split(",")
+        CONFIGS[f"custom_{sc}_{w}x{h}_spp{spp}_d{depth}"] = dict(scene=sc, w=int(w), h=int(h), spp=int(spp), depth=int(depth))
+    names = [n for n in CONFIGS if (not a.only and not a.custom) or (a.only and any(o in n for o in a.only.split(",")))
+             or (a.custom and n.startswith("custom_"))]
     out = {}
     for n in names:
         out[n] = run(CONFIGS[n], a.frames, a.warmup)

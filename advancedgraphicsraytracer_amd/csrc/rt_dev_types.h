@@ -54,6 +54,8 @@ struct FrameArgs {
     float lens, rw, rh;
     uint32_t W, H, spp, depth, frame, reset;
     uint32_t shard, nshards, tiles_x, ntiles_local;
+    uint32_t nchunks, nunits;           // sample chunks per tile (1 = no split); ntiles_local * nchunks
+    float4 *samples;                    // nchunks > 1: per-sample values [spp][ntiles_local][64]
     int packed_out;
     float4 *acc;
     uint32_t *out;

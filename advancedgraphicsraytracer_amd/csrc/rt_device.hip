@@ -65,6 +65,7 @@ struct rt_scene {
     uint32_t pt_drain_level = 64;   // bounce level from which the wavefront always drains (64 = never forced)
     double pt_drain_rounds = 1.0;   // ... and it drains any level holding <= this many rounds of resident lanes
     bool pt_full_grid = false;      // levels >= 1: one wave per queue slot group instead of a resident grid
+    uint32_t split_units = 16000;   // sample split target: about 4 rounds of the 4096 resident waves
     uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per renderer: 12 GB of the 288 GB HBM
                                               // holds all 16 spp of a 1080p depth-10 frame
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
@@ -90,6 +91,9 @@ struct rt_renderer {
     // wavefront path tracer (PathArgs): one allocation, grown on demand
     void *d_pt = nullptr;
     size_t pt_bytes = 0;
+    // per-sample values of sample-split frames (FrameArgs::samples)
+    void *d_samples = nullptr;
+    size_t samples_bytes = 0;
 };
 
 namespace {
@@ -478,6 +482,8 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_PT_DRAIN_LEVEL")) s->pt_drain_level = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_DRAIN_ROUNDS")) s->pt_drain_rounds = std::max(0.0, std::atof(e));
     if (const char *e = std::getenv("RT_PT_FULL_GRID")) s->pt_full_grid = std::atoi(e) != 0;
+    // RT_SPLIT_UNITS: sample-split target units (0 = never split)
+    if (const char *e = std::getenv("RT_SPLIT_UNITS")) s->split_units = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
@@ -532,8 +538,11 @@ uint64_t frame_pixels(const rt_renderer *r, const FrameArgs &F, uint32_t shard, 
 // Wavefront path tracing of one frame / shard (PathArgs, rt_dev_types.h): the samples are
 // processed in batches that fit RT_PT_MEM_MB (default 12288 MB) of path state; per batch
 // one k_pt_level launch per bounce level, then k_pt_finish.
-int launch_pt_frame(rt_renderer *r, const FrameArgs &F, const SceneView &view, bool tex, hipStream_t st) {
+int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex, hipStream_t st) {
     rt_scene *s = r->scene;
+    // camera rays of level 0 take the wave-coherent walk when the scene forces it, or when
+    // the renderer's primary+shadow frames timed it faster (RT_WALK_AUTO)
+    view.wave_primary = !s->has_cubes && (s->walk == RT_WALK_WAVE || (s->walk == RT_WALK_AUTO && r->tune == 4 && r->wave));
     const uint64_t npix = (uint64_t)F.ntiles_local * 64u;
     const uint64_t per_path = 32u + 16u + 8u + (uint64_t)(F.depth - 1) * 32u;
     const uint64_t budget = s->pt_mem_bytes;
@@ -620,22 +629,48 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     const bool tex = !s->view.sky_const;
     const int mode = (int)p->mode;
     const int lds_kind = lds_kind_for(s, mode, md);
+    // sample split: a frame (or a shard of one) with few tiles and several samples per
+    // pixel is cut into (tile, sample chunk) units, so the dispatcher still balances about
+    // s->split_units waves of uneven cost (a 1/8 shard at spp 8 would otherwise be one
+    // round of whole-tile waves, as long as its slowest tile)
+    F.nchunks = 1;
+    const bool wavefront = mode == RT_MODE_PATH && depth >= 2 && s->pt_wavefront;
+    // (measured on TEAPOT-F shards, tools/shard_time.py: no split while the tiles alone make
+    // ~4 rounds; below that, split until ~8 rounds, chunks of equal sample counts)
+    if (p->spp > 1 && mode != RT_MODE_PACKET && !wavefront && F.ntiles_local < s->split_units)
+        while (F.ntiles_local * F.nchunks < 2u * s->split_units && F.nchunks < p->spp) {
+            uint32_t d = F.nchunks + 1;                  // next divisor of spp: equal chunks
+            while (p->spp % d) ++d;
+            F.nchunks = d;
+        }
+    F.nunits = F.ntiles_local * F.nchunks;
+    if (F.nchunks > 1) {
+        const size_t need = sizeof(float4) * (size_t)p->spp * F.ntiles_local * 64u;
+        if (need > r->samples_bytes) {
+            if (r->d_samples) HIP_TRY(hipFree(r->d_samples));
+            r->d_samples = nullptr;
+            r->samples_bytes = 0;
+            HIP_TRY(hipMalloc(&r->d_samples, need));
+            r->samples_bytes = need;
+        }
+        F.samples = static_cast<float4 *>(r->d_samples);
+    }
     dim3 grid, block;
     size_t lds;
     if (lds_kind == 64) {
-        grid = dim3((F.ntiles_local + RT_LDS_WG_TILES - 1) / RT_LDS_WG_TILES);
+        grid = dim3((F.nunits + RT_LDS_WG_TILES - 1) / RT_LDS_WG_TILES);
         block = dim3(1024);
         lds = lds_scene_bytes(s);
     } else if (lds_kind == 48) {
-        grid = dim3((F.ntiles_local + 7) / 8);
+        grid = dim3((F.nunits + 7) / 8);
         block = dim3(512);
         lds = lds48_scene_bytes(s);
     } else {
-        grid = dim3((F.ntiles_local + 3) / 4);
+        grid = dim3((F.nunits + 3) / 4);
         block = dim3(256);
         lds = stack_bytes(s);
     }
-    if (mode == RT_MODE_PATH && depth >= 2 && s->pt_wavefront) {
+    if (wavefront) {
         int rc = launch_pt_frame(r, F, s->view, tex, st);
         if (rc != RT_OK) return rc;
         r->primary += frame_pixels(r, F, shard, nshards, tiles_x, ntiles) * p->spp;
@@ -672,6 +707,14 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     else kcore::launch_frame(view, F, L);
     HIP_TRY(hipGetLastError());
     if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed + 1], st));
+    if (F.nchunks > 1) {   // the pixels' samples in sample order, running average, RGB8
+        PathArgs P{};
+        P.batch_spp = p->spp;
+        P.result = F.samples;
+        if (s->ext) kext::launch_pt_finish(F, P, true, st);
+        else kcore::launch_pt_finish(F, P, true, st);
+        HIP_TRY(hipGetLastError());
+    }
     (void)tiles_y;
     r->primary += frame_pixels(r, F, shard, nshards, tiles_x, ntiles) * p->spp;
     r->frames += 1;
@@ -848,6 +891,7 @@ int rt_renderer_destroy(rt_renderer *r) {
     (void)hipFree(r->d_counters);
     if (r->d_rgb) (void)hipFree(r->d_rgb);
     if (r->d_pt) (void)hipFree(r->d_pt);
+    if (r->d_samples) (void)hipFree(r->d_samples);
     for (auto &e : r->tev)
         if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(r->stream);

@@ -1,0 +1,124 @@
+"""Hand-made scenes shared by the parity tests and the fixture generator: the same
+primitive list built in the oracle (the checker), and the primitive known-answer set
+(edge, vertex, grazing, parallel, inside-sphere, t ~ EPS, exact ties, NaN slabs)."""
+import numpy as np
+
+
+def oracle_scene(rt, oracle, prims, mats, sky=None, textures=()):
+    """The primitive list (rt.sphere / plane / triangle / cube / quad records) as an oracle scene."""
+    import ctypes as C
+    L = oracle.lib()
+    h = L.or_scene_new()
+    f3 = lambda *v: (C.c_float * 3)(*v)
+    f16 = lambda T: (C.c_float * 16)(*(np.eye(4, dtype=np.float32).reshape(16) if T is None else T))
+    for t in textures:
+        t = np.ascontiguousarray(t, np.uint32)
+        L.or_scene_add_texture(h, t.shape[1], t.shape[0], t.ctypes.data_as(C.POINTER(C.c_uint32)))
+    for m in mats:
+        L.or_scene_add_material_tex(h, m.kind, f3(*m.color), f3(*m.color2), m.ior, m.diffuse, m.texture)
+    for p in prims:
+        v = list(p.v)
+        if p.type == rt.SPHERE:
+            L.or_scene_add_sphere(h, f3(*v[:3]), v[3], p.material)
+        elif p.type == rt.PLANE:
+            L.or_scene_add_plane(h, f3(*v[:3]), v[3], p.material)
+        elif p.type == rt.CUBE:
+            L.or_scene_add_cube(h, f3(*v[:3]), f3(*v[3:6]), f16(getattr(p, "T", None)), p.material)
+        elif p.type == rt.QUAD:
+            L.or_scene_add_quad(h, v[0], f16(getattr(p, "T", None)), p.material)
+        else:
+            L.or_scene_add_triangle(h, f3(*v[:3]), f3(*v[3:6]), f3(*v[6:9]), p.material)
+    if sky is not None:
+        L.or_scene_set_sky(h, sky.shape[1], sky.shape[0], sky.ctypes.data_as(C.POINTER(C.c_uint32)))
+    L.or_scene_build_bvh(h)
+    o = oracle.Scene.__new__(oracle.Scene)
+    o.L, o.h = L, h
+    return o
+
+
+
+
+# ---- primitive known-answer set (Primitive.h:64-314, scene.h:285-487)
+EPS = np.float32(1e-4)
+
+
+def kat_scene(rt):
+    """Light (prim 0), two triangles sharing an edge, two coincident triangles (exact ties),
+    two spheres, a plane (outside the BVH: AABB +-1e30, Primitive.h:322-323)."""
+    mats = [rt.material(rt.LIGHT, (24, 24, 22)), rt.material(rt.DIFFUSE, (0.8, 0.8, 0.8)),
+            rt.material(rt.MIRROR, (0.9, 0.9, 0.9))]
+    prims = [rt.sphere((0, 4, -2), 0.5, 0),
+             rt.triangle((0, 0, 5), (1, 0, 5), (0, 1, 5), 1),          # 1: T1
+             rt.triangle((1, 0, 5), (1, 1, 5), (0, 1, 5), 1),          # 2: T2, shares T1's hypotenuse
+             rt.triangle((-2, -1, 7), (-1, -1, 7), (-2, 0, 7), 1),     # 3: T3a
+             rt.triangle((-2, -1, 7), (-1, -1, 7), (-2, 0, 7), 2),     # 4: T3b == T3a (tie)
+             rt.sphere((3, 0, 5), 1.0, 2),                             # 5: S1
+             rt.sphere((-3, 2, 5), 0.25, 1),                           # 6: S2
+             rt.plane((0, 1, 0), 2.0, 1)]                              # 7: y = -2
+    return prims, mats
+
+
+def _ray(o, d, tmax=1e34):
+    return [np.float32(o[0]), np.float32(o[1]), np.float32(o[2]), np.float32(d[0]), np.float32(d[1]),
+            np.float32(d[2]), np.float32(tmax)]
+
+
+def kat_rays():
+    """Hand-picked rays (7 floats: O, D, tmax) + a jittered cloud around the vertices/edges."""
+    up = 1.0 / np.sqrt(np.float32(2))
+    R = []
+    # T1 / T2: vertices, shared edge (tie between 1 and 2), edges, just outside, centre
+    for p in [(0, 0), (1, 0), (0, 1), (1, 1), (0.5, 0.5), (0.25, 0.75), (0.5, 0), (0, 0.5), (1, 0.5), (0.5, 1),
+              (0.3, 0.3), (1.0000001, 0.5), (-1e-7, 0.5), (0.5, -1e-7)]:
+        R.append(_ray((p[0], p[1], 0), (0, 0, 1)))
+        R.append(_ray((p[0], p[1], 10), (0, 0, -1)))                  # back faces (no culling)
+    # ray in the triangles' plane, grazing rays
+    R.append(_ray((-1, 0.2, 5), (1, 0, 0)))
+    R.append(_ray((-1, 0.2, 4.999), (1, 0, 1e-4)))
+    R.append(_ray((0.2, 0.2, 4), (0, 1e-7, 1)))
+    # t around EPS (t > EPS strict, Primitive.h:270)
+    for dz in (1e-4, 9.9e-5, 1.01e-4, 2e-4, 0.0, -1e-5):
+        R.append(_ray((0.2, 0.2, np.float32(5) - np.float32(dz)), (0, 0, 1)))
+    # exact duplicate triangles: tie -> first tested wins
+    for p in [(-1.8, -0.8), (-1.5, -0.5), (-2, -1), (-1, -1), (-2, 0)]:
+        R.append(_ray((p[0], p[1], 0), (0, 0, 1)))
+    # S1: centre inside (second root), tangent, origin on the surface, just outside, t ~ EPS
+    R.append(_ray((3, 0, 5), (0, 0, 1)))
+    R.append(_ray((3, 0, 5), (up, up, 0)))
+    R.append(_ray((4, -5, 5), (0, 1, 0)))                           # tangent at x = 4
+    R.append(_ray((4.0000005, -5, 5), (0, 1, 0)))
+    R.append(_ray((3, 0, 4), (0, 0, 1)))                            # starts on the surface
+    R.append(_ray((3, 0, np.float32(4) - np.float32(1e-4)), (0, 0, 1)))
+    R.append(_ray((3, 0, 0), (0, 0, 1)))
+    R.append(_ray((3, 0, 10), (0, 0, -1)))
+    R.append(_ray((-3, 2, 0), (0, 0, 1)))
+    # plane y = -2: from above, from below, parallel, in the plane
+    R.append(_ray((0, 0, 0), (0, -1, 0)))
+    R.append(_ray((0, -3, 0), (0, 1, 0)))
+    R.append(_ray((0, -1, 0), (1, 0, 0)))
+    R.append(_ray((0, -2, 0), (1, 0, 0)))
+    R.append(_ray((0, -2, 0), (0, -1, 0)))
+    # axis-parallel rays with origins on node slab planes: (slab - O) * inf = NaN
+    for o in [(0, 0.5, 0), (1, 0.5, 0), (0.5, 0, 0), (0.5, 1, 0), (0, 0, 0), (-2, -1, 0), (4, 0, 0)]:
+        R.append(_ray(o, (0, 0, 1)))
+        R.append(_ray(o, (0, 0, -1)))
+        R.append(_ray((o[0], o[1], 5), (1, 0, 0)))
+        R.append(_ray((o[0], o[1], 5), (-0.0, 1, 0)))
+    # shadow-style rays whose tmax ends exactly at / just before / after a surface
+    for tm in (5.0, 4.9999995, 5.0000005, 5.0 - 2e-4):
+        R.append(_ray((0.2, 0.2, 0), (0, 0, 1), tm))
+        R.append(_ray((3, 0, -2), (0, 0, 1), tm))
+    rays = np.array(R, np.float32)
+    # jittered cloud: rays from random points toward the vertices / edge points +- a few ulps
+    rng = np.random.default_rng(2024)
+    targets = np.array([[0, 0, 5], [1, 0, 5], [0, 1, 5], [1, 1, 5], [0.5, 0.5, 5], [-2, -1, 7], [-1, -1, 7],
+                        [-2, 0, 7], [3, 1, 5], [4, 0, 5], [-3, 2.25, 5]], np.float32)
+    n = 4000
+    O = rng.uniform(-4, 4, (n, 3)).astype(np.float32)
+    O[:, 2] = rng.uniform(-3, 1, n).astype(np.float32)
+    T = targets[rng.integers(0, len(targets), n)]
+    T = T + rng.integers(-3, 4, (n, 3)).astype(np.float32) * np.float32(1.2e-7)   # a few ulps off
+    D = (T - O).astype(np.float32)
+    D /= np.linalg.norm(D, axis=1, keepdims=True).astype(np.float32)
+    cloud = np.concatenate([O, D.astype(np.float32), np.full((n, 1), 1e34, np.float32)], 1).astype(np.float32)
+    return np.concatenate([rays, cloud], 0)

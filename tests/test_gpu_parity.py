@@ -8,6 +8,8 @@ import os
 import numpy as np
 import pytest
 
+from scenes_util import oracle_scene
+
 pytestmark = pytest.mark.gpu
 
 PIX_TOL = 1e-4   # north_star: pixel output within 1e-4
@@ -188,37 +190,6 @@ def twin_scene(rt, oracle, prims, mats, sky=None, textures=()):
     """The same hand-made scene in the product (device) and in the oracle."""
     o = oracle_scene(rt, oracle, prims, mats, sky, textures)
     return rt.Scene(prims, mats, sky=sky, textures=textures), o
-
-
-def oracle_scene(rt, oracle, prims, mats, sky=None, textures=()):
-    import ctypes as C
-    L = oracle.lib()
-    h = L.or_scene_new()
-    f3 = lambda *v: (C.c_float * 3)(*v)
-    f16 = lambda T: (C.c_float * 16)(*(np.eye(4, dtype=np.float32).reshape(16) if T is None else T))
-    for t in textures:
-        t = np.ascontiguousarray(t, np.uint32)
-        L.or_scene_add_texture(h, t.shape[1], t.shape[0], t.ctypes.data_as(C.POINTER(C.c_uint32)))
-    for m in mats:
-        L.or_scene_add_material_tex(h, m.kind, f3(*m.color), f3(*m.color2), m.ior, m.diffuse, m.texture)
-    for p in prims:
-        v = list(p.v)
-        if p.type == rt.SPHERE:
-            L.or_scene_add_sphere(h, f3(*v[:3]), v[3], p.material)
-        elif p.type == rt.PLANE:
-            L.or_scene_add_plane(h, f3(*v[:3]), v[3], p.material)
-        elif p.type == rt.CUBE:
-            L.or_scene_add_cube(h, f3(*v[:3]), f3(*v[3:6]), f16(getattr(p, "T", None)), p.material)
-        elif p.type == rt.QUAD:
-            L.or_scene_add_quad(h, v[0], f16(getattr(p, "T", None)), p.material)
-        else:
-            L.or_scene_add_triangle(h, f3(*v[:3]), f3(*v[3:6]), f3(*v[6:9]), p.material)
-    if sky is not None:
-        L.or_scene_set_sky(h, sky.shape[1], sky.shape[0], sky.ctypes.data_as(C.POINTER(C.c_uint32)))
-    L.or_scene_build_bvh(h)
-    o = oracle.Scene.__new__(oracle.Scene)
-    o.L, o.h = L, h
-    return o
 
 
 def sky_scene(rt, oracle, make=twin_scene):

@@ -869,8 +869,8 @@ int rt_renderer_create(rt_scene *s, uint32_t W, uint32_t H, rt_renderer **out) {
     hipError_t e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&r->d_acc, sizeof(float4) * (size_t)W * H);   // Renderer::Init, renderer.cpp:6-12
     if (e == hipSuccess) e = hipMemsetAsync(r->d_acc, 0, sizeof(float4) * (size_t)W * H, r->stream);
-    if (e == hipSuccess) e = hipMalloc(&r->d_counters, 4 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemsetAsync(r->d_counters, 0, 4 * sizeof(unsigned long long), r->stream);
+    if (e == hipSuccess) e = hipMalloc(&r->d_counters, kCounterSlots * 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemsetAsync(r->d_counters, 0, kCounterSlots * 8 * sizeof(unsigned long long), r->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(r->stream);   // ready before any caller stream uses it
     if (e != hipSuccess) {
         if (r->d_acc) (void)hipFree(r->d_acc);
@@ -942,11 +942,15 @@ int rt_renderer_counters(rt_renderer *r, rt_counters *out) {
     if (!r || !out) return fail(RT_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(r->scene->device));
     HIP_TRY(hipDeviceSynchronize());
-    unsigned long long c[4];
-    HIP_TRY(hipMemcpy(c, r->d_counters, sizeof(c), hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> c((size_t)kCounterSlots * 8);
+    HIP_TRY(hipMemcpy(c.data(), r->d_counters, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     out->primary = r->primary;
-    out->shadow = c[0];
-    out->bounce = c[1];
+    out->shadow = 0;
+    out->bounce = 0;
+    for (uint32_t k = 0; k < kCounterSlots; ++k) {
+        out->shadow += c[(size_t)k * 8];
+        out->bounce += c[(size_t)k * 8 + 1];
+    }
     out->frames = r->frames;
     return RT_OK;
 }

@@ -91,8 +91,15 @@ struct FrameLaunch {
 // queue_in / queue_out: path indices alive at this level / the next; qcount[level] their
 // counts (level 0 = every path of the batch, no queue).  sum: the per-pixel running sum
 // over the samples of earlier batches (sample order kept).
+// The level queues are kQueueSegs segments of seg_cap entries, each with its own count
+// (64 B apart): a wave appends its survivors to segment (chunk index % kQueueSegs), so
+// the per-wave atomics spread over kQueueSegs addresses instead of serialising on one.
+// qcount[(level * kQueueSegs + k) * 16] = entries of segment k at that level.
+constexpr uint32_t kQueueSegs = 16;
+
 struct PathArgs {
     uint32_t s0, batch_spp, npaths, level;
+    uint32_t seg_cap;                    // entries per queue segment
     uint32_t drain_level, drain_below;   // drain (run every remaining level) from this level on /
                                          // at any level holding at most this many paths
     float4 *state;

@@ -550,7 +550,12 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     batch = std::min<uint64_t>(batch, F.spp);
     if (batch * npix > 0xffffffffull / 2) batch = std::max<uint64_t>(1, (0xffffffffull / 2) / npix);
     const uint64_t np = batch * npix;
-    const size_t need = (size_t)(np * per_path + npix * 16u + 64u * 4u + 4096u);
+    // queue segment k takes the survivors of chunks j = k (mod kQueueSegs); the grid's
+    // wave count is a multiple of kQueueSegs, so a segment never gets more than this
+    const uint64_t seg_cap = ((np / 64u + kQueueSegs - 1) / kQueueSegs + 1) * 64u;
+    const size_t qbytes = (size_t)seg_cap * kQueueSegs * 4u;
+    const size_t cbytes = (size_t)(F.depth + 1) * kQueueSegs * 64u;
+    const size_t need = (size_t)(np * (per_path - 8u) + 2 * qbytes + npix * 16u + cbytes + 4096u);
     if (need > r->pt_bytes) {
         if (r->d_pt) HIP_TRY(hipFree(r->d_pt));
         r->d_pt = nullptr;
@@ -563,10 +568,11 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     PathArgs P{};
     P.state = reinterpret_cast<float4 *>(take(np * 32u));
     P.result = reinterpret_cast<float4 *>(take(np * 16u));
-    uint32_t *q0 = reinterpret_cast<uint32_t *>(take(np * 4u));
-    uint32_t *q1 = reinterpret_cast<uint32_t *>(take(np * 4u));
+    uint32_t *q0 = reinterpret_cast<uint32_t *>(take(qbytes));
+    uint32_t *q1 = reinterpret_cast<uint32_t *>(take(qbytes));
     P.sum = reinterpret_cast<float4 *>(take(npix * 16u));
-    P.qcount = reinterpret_cast<uint32_t *>(take(64u * 4u));
+    P.qcount = reinterpret_cast<uint32_t *>(take(cbytes));
+    P.seg_cap = (uint32_t)seg_cap;
     P.rec = reinterpret_cast<float4 *>(take((size_t)(F.depth - 1) * np * 32u));
     const size_t lds = stack_bytes(s);
     // levels are compacted level by level until one is small enough to drain (k_pt_level)
@@ -577,7 +583,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         P.s0 = s0;
         P.batch_spp = std::min<uint32_t>((uint32_t)batch, F.spp - s0);
         P.npaths = (uint32_t)(P.batch_spp * npix);
-        HIP_TRY(hipMemsetAsync(P.qcount, 0, 64u * 4u, st));
+        HIP_TRY(hipMemsetAsync(P.qcount, 0, cbytes, st));
         for (uint32_t level = 0; level < F.depth; ++level) {
             P.level = level;
             P.queue_in = (level & 1u) ? q1 : q0;

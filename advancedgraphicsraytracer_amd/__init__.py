@@ -17,7 +17,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "librtamd.so")
+LIB_PATH = os.path.abspath(os.environ.get("RTAMD_LIB", os.path.join(PKG_DIR, "librtamd.so")))   # RTAMD_LIB: A/B builds (tools/)
 DATA_DIR = os.path.join(PKG_DIR, "data")
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "rt_amd.h")
 

@@ -65,7 +65,7 @@ struct rt_scene {
     uint32_t pt_drain_level = 64;   // bounce level from which the wavefront always drains (64 = never forced)
     double pt_drain_rounds = 1.0;   // ... and it drains any level holding <= this many rounds of resident lanes
     bool pt_full_grid = false;      // levels >= 1: one wave per queue slot group instead of a resident grid
-    uint32_t split_units = 16000;   // sample split target: about 4 rounds of the 4096 resident waves
+    uint32_t split_units = 20000;   // sample split below ~5 rounds of the 4096 resident waves
     uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per renderer: 12 GB of the 288 GB HBM
                                               // holds all 16 spp of a 1080p depth-10 frame
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
@@ -642,7 +642,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     F.nchunks = 1;
     const bool wavefront = mode == RT_MODE_PATH && depth >= 2 && s->pt_wavefront;
     // (measured on TEAPOT-F shards, tools/shard_time.py: no split while the tiles alone make
-    // ~4 rounds; below that, split until ~8 rounds, chunks of equal sample counts)
+    // ~5 rounds; below that, split until ~10 rounds, chunks of equal sample counts)
     if (p->spp > 1 && mode != RT_MODE_PACKET && !wavefront && F.ntiles_local < s->split_units)
         while (F.ntiles_local * F.nchunks < 2u * s->split_units && F.nchunks < p->spp) {
             uint32_t d = F.nchunks + 1;                  // next divisor of spp: equal chunks

@@ -464,12 +464,14 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     }
     v.stack_entries = s->stack_depth;
     v.node_f4 = 2u * s->bvh.nodes_used;
-    // LDS kernels, preferred in this order: two 512-thread workgroups per CU (k_render_lds48)
-    // when half the LDS holds the 48-B pairs, words and u16 stacks; one 1024-thread group
-    // (k_render_lds) when the 64-B pairs and u32 stacks fit; else global nodes.
-    // RT_LDS_KERNEL=48/64/0 overrides (A/B runs).
-    if (lds48_scene_bytes(s) <= 80u * 1024u) s->lds_kernel = 48;
-    else if ((size_t)s->stack_depth * 4096u + (size_t)s->bvh.nodes_used * 32u <= 160u * 1024u) s->lds_kernel = 64;
+    // Primary+shadow frames read the nodes from global memory (L1/L2-resident, 256-thread
+    // workgroups, 5 waves/SIMD).  The LDS-node kernels -- two 512-thread workgroups per CU
+    // holding the 48-B pairs, words and u16 stacks (k_render_lds48), or one 1024-thread
+    // group with the 64-B pairs (k_render_lds) -- are opt-in (RT_LDS_KERNEL=48/64): they
+    // won while every wave's ray counter went to one atomic address, and lose by 12 % since
+    // (TEAPOT-F 0.169 vs 0.192 ms, profiles/r01/ab_kernel_choice_*.json; LDS occupancy caps
+    // them at 4 waves/SIMD).
+    s->lds_kernel = 0;
     if (const char *e = std::getenv("RT_LDS_KERNEL")) {
         const int k = std::atoi(e);
         if (k == 0 || (k == 64 && (size_t)s->stack_depth * 4096u + (size_t)s->bvh.nodes_used * 32u <= 160u * 1024u) ||

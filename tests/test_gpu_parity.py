@@ -424,7 +424,7 @@ def test_frame_kernel_name(rt):
     """rt_frame_kernel_name names the kernel the bench's roofline line is about."""
     s = rt.Scene.recipe("teapotF")
     r = rt.Renderer(s, 64, 64)
-    assert r.kernel_name(spp=1, depth=1) == "k_render_lds48<1>"
+    assert r.kernel_name(spp=1, depth=1) == "k_render<path,1>"
     assert r.kernel_name(spp=1, depth=10) == "k_pt_level"
     r.mode = rt.MODE_WHITTED
     assert r.kernel_name(spp=1, depth=5) == "k_render<whitted,1>"
@@ -493,3 +493,35 @@ def test_sample_split_equals_whole_tiles(rt, torch, monkeypatch, recipe, W, H, s
         assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
     assert np.array_equal(ra.accumulator(), rb.accumulator())
     assert ra.counters() == rb.counters()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["48", "64"])
+@pytest.mark.parametrize("spp,shards", [(1, 1), (4, 3)])
+def test_lds_node_kernels_equal_global_kernel(rt, torch, monkeypatch, kind, spp, shards):
+    """The opt-in LDS-node primary+shadow kernels (RT_LDS_KERNEL=48: 48-B pairs + u16
+    stacks, 2 x 512 threads; 64: 64-B pairs, 1024 threads) must give the global-node
+    kernel's frames bit for bit (whole frames and sample-split shards)."""
+    W, H = 200, 120
+    monkeypatch.setenv("RT_LDS_KERNEL", "0")
+    s_g = rt.Scene.recipe("teapotF")
+    monkeypatch.setenv("RT_LDS_KERNEL", kind)
+    s_l = rt.Scene.recipe("teapotF")
+    rg, rl = rt.Renderer(s_g, W, H), rt.Renderer(s_l, W, H)
+    assert rg.kernel_name(spp=spp, depth=1) == "k_render<path,1>"
+    assert rl.kernel_name(spp=spp, depth=1) == ("k_render_lds48<1>" if kind == "48" else "k_render_lds<1>")
+    dev = torch.device("cuda", 0)
+    for f in range(2):
+        if shards == 1:
+            a, b = rg.tick_host(spp=spp, depth=1, frame=f), rl.tick_host(spp=spp, depth=1, frame=f)
+        else:
+            cap = rg.shard_capacity(shards)
+            ta = torch.zeros(cap, dtype=torch.int32, device=dev)
+            tb = torch.zeros(cap, dtype=torch.int32, device=dev)
+            rg.render_shard(ta, 2, shards, spp=spp, depth=1, frame=f)
+            rl.render_shard(tb, 2, shards, spp=spp, depth=1, frame=f)
+            torch.cuda.synchronize()
+            a, b = ta.cpu().numpy(), tb.cpu().numpy()
+        assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
+    assert np.array_equal(rg.accumulator(), rl.accumulator())
+    assert rg.counters() == rl.counters()

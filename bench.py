@@ -181,7 +181,12 @@ def main():
             roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                         "kernel": rend.kernel_name(spp=spp, depth=args.depth), "kernel_ms": round(kern_ms, 4),
-                        "bytes_per_ray": {"primary": round(bp, 1), "shadow": round(bs, 1)}}
+                        "bytes_per_ray": {"primary": round(bp, 1), "shadow": round(bs, 1)},
+                        # the algorithmic node / triangle bytes are served by L1/L2 (the scene is
+                        # ~0.1 MB): frac > 1 means "beyond the HBM roofline"; the HBM bytes the
+                        # PMC counters see per launch, and their rate, are these
+                        "hbm_measured_gbs": round(traffic / (kern_ms * 1e-3) / 1e9, 2) if traffic else None,
+                        "hbm_measured_frac": round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if traffic else None}
         line = {
             "metric": "Mrays/s (primary+shadow) at 1080p",
             "value": round(tot_rays / wall / 1e6, 3),

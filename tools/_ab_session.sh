@@ -1,5 +1,7 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 300 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
-timeout -k 10 200 python tools/shard_time.py > gpurun_out/shard_final.log 2>&1
-timeout -k 10 240 python tools/configs.py --json gpurun_out/configs.json > gpurun_out/configs.log 2>&1
+V=variants/xcd.so
+timeout -k 10 200 python tools/ab.py $V@RT_XCD_REMAP=0 $V --scene mig16 --rounds 7 --frames 20 --check > gpurun_out/ab_xcd_mig.json
+timeout -k 10 200 python tools/ab.py $V@RT_XCD_REMAP=0 $V --scene teapotF --rounds 7 --frames 20 --check > gpurun_out/ab_xcd_tp.json
+timeout -k 10 200 python tools/ab.py $V@RT_XCD_REMAP=0 $V --scene cfg5 --rounds 7 --frames 20 --check > gpurun_out/ab_xcd_cfg5.json
+timeout -k 10 200 python tools/ab.py $V@RT_XCD_REMAP=0 $V --scene cfg3 --rounds 7 --frames 20 --check > gpurun_out/ab_xcd_cfg3.json

@@ -62,6 +62,8 @@ struct FrameArgs {
     uint32_t nchunks, nunits;           // sample chunks per tile (1 = no split); ntiles_local * nchunks
     float4 *samples;                    // nchunks > 1: per-sample values [spp][ntiles_local][64]
     int packed_out;
+    const uint32_t *order;              // tile dispatch order: local tile of slot i (nullptr = identity)
+    uint32_t *tile_cost;                // if set: each tile's wave cycles (to build the order)
     float4 *acc;
     uint32_t *out;
     unsigned long long *counters;       // kCounterSlots slots of 8 u64 (64 B): [0] shadow rays, [1] bounce rays

@@ -65,6 +65,7 @@ struct rt_scene {
     uint32_t pt_drain_level = 64;   // bounce level from which the wavefront always drains (64 = never forced)
     double pt_drain_rounds = 1.0;   // ... and it drains any level holding <= this many rounds of resident lanes
     bool pt_full_grid = false;      // levels >= 1: one wave per queue slot group instead of a resident grid
+    bool tile_order = true;         // measured-cost (longest first) tile order (RT_TILE_ORDER=0: off)
     uint32_t split_units = 20000;   // sample split below ~5 rounds of the 4096 resident waves
     uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per renderer: 12 GB of the 288 GB HBM
                                               // holds all 16 spp of a 1080p depth-10 frame
@@ -85,6 +86,12 @@ struct rt_renderer {
     hipStream_t stream = nullptr;
     // RT_WALK_AUTO: the first eligible frames time the lane walk and the wave walk on the
     // caller's stream (one warm-up, one each), the fourth picks the faster for good
+    // measured-cost tile order (tile_order_step): per-tile cycles of one frame (two cost
+    // maps while the camera walk is being timed), longest tile first afterwards
+    uint32_t *d_order = nullptr, *d_cost = nullptr;
+    uint32_t order_n = 0;
+    uint64_t order_key = 0;
+    int order_state = 0;        // 0 idle, 1 costs recorded, 2 order active
     int tune = 0;
     bool wave = false;
     hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -484,6 +491,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_PT_DRAIN_LEVEL")) s->pt_drain_level = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_DRAIN_ROUNDS")) s->pt_drain_rounds = std::max(0.0, std::atof(e));
     if (const char *e = std::getenv("RT_PT_FULL_GRID")) s->pt_full_grid = std::atoi(e) != 0;
+    if (const char *e = std::getenv("RT_TILE_ORDER")) s->tile_order = std::atoi(e) != 0;
     // RT_SPLIT_UNITS: sample-split target units (0 = never split)
     if (const char *e = std::getenv("RT_SPLIT_UNITS")) s->split_units = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
@@ -603,6 +611,62 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     return RT_OK;
 }
 
+// Longest-tile-first dispatch (LPT): tiles differ in cost by an order of magnitude (sky vs
+// mesh), and the dispatcher hands out workgroups in index order, so expensive tiles that come
+// last leave most CUs idle at the end of the frame.  Each tile's wave cycles are recorded on
+// one frame, sorted on the host once, and from the next frame on slot i renders the i-th most
+// expensive tile -- for as long as camera, size, spp, depth, mode and shard stay the same.
+// With the RT_WALK_AUTO camera walk still being timed, the two timed frames record the costs
+// under each walk and the frame that picks the walk applies the matching order (active from
+// the 4th frame); otherwise frame 1 records and frame 2 applies.  Pixel values do not depend
+// on the order.  walk_phase: -1 no walk timing pending, 0 / 1 this frame times the lane /
+// wave walk, 2 the walk was picked on this frame, 3 the timing has not started yet.
+int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt_frame_params *p, int walk_phase) {
+    uint64_t key = 1469598103934665603ull;
+    auto mix = [&](const void *d, size_t n) {
+        const unsigned char *c = static_cast<const unsigned char *>(d);
+        for (size_t i = 0; i < n; ++i) key = (key ^ c[i]) * 1099511628211ull;
+    };
+    mix(cam, sizeof(*cam));
+    mix(&p->width, sizeof(uint32_t) * 4);   // width height spp depth
+    mix(&p->mode, sizeof(uint32_t));
+    mix(&F.shard, sizeof(uint32_t) * 2);    // shard nshards
+    const uint32_t n = F.ntiles_local;
+    if (key != r->order_key || n != r->order_n) {
+        r->order_key = key;
+        r->order_state = 0;
+        if (n != r->order_n) {
+            if (r->d_order) HIP_TRY(hipFree(r->d_order));
+            if (r->d_cost) HIP_TRY(hipFree(r->d_cost));
+            r->d_order = r->d_cost = nullptr;
+            r->order_n = 0;
+            HIP_TRY(hipMalloc(&r->d_order, n * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&r->d_cost, 2u * n * sizeof(uint32_t)));   // one cost map per camera walk
+            r->order_n = n;
+        }
+    }
+    int use = -1;                                                      // cost map to sort this frame
+    if (walk_phase == 3) {
+        // walk timing not started yet: record nothing
+    } else if (r->order_state == 0) {
+        if (walk_phase == 0 || walk_phase == 1) F.tile_cost = r->d_cost + (size_t)walk_phase * n;
+        else if (walk_phase == 2) use = r->wave ? 1 : 0;              // recorded on the timed frames
+        else { F.tile_cost = r->d_cost; r->order_state = 1; }
+    } else if (r->order_state == 1) {
+        use = 0;
+    }
+    if (use >= 0) {
+        std::vector<uint32_t> cost(n), ord(n);
+        HIP_TRY(hipMemcpy(cost.data(), r->d_cost + (size_t)use * n, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; ++i) ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+        HIP_TRY(hipMemcpy(r->d_order, ord.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+        r->order_state = 2;
+    }
+    if (r->order_state == 2) F.order = r->d_order;
+    return RT_OK;
+}
+
 int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
                   uint32_t *out, int packed, void *stream) {
     if (!r || !cam || !p || !out) return fail(RT_ERR_INVALID, "rt_render: null argument");
@@ -690,6 +754,8 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     // camera-ray walk (only the global-node primary+shadow kernel has both)
     const bool walk_kernel = mode == RT_MODE_PATH && md == 1 && lds_kind == 0 && !s->ext;
     int timed = -1;   // tev pair recorded around this launch
+    bool walk_decided = false;
+    const bool walk_pending = walk_kernel && s->walk == RT_WALK_AUTO && r->tune < 4;
     if (walk_kernel) {
         if (s->walk == RT_WALK_WAVE) view.wave_primary = 1;
         else if (s->walk == RT_WALK_AUTO) {
@@ -706,9 +772,14 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
                 HIP_TRY(hipEventElapsedTime(&tw, r->tev[2], r->tev[3]));
                 r->wave = tw < tl;
                 r->tune = 4;
+                walk_decided = true;
             }
             if (r->tune == 4) view.wave_primary = r->wave ? 1 : 0;
         }
+    }
+    if (s->tile_order) {
+        const int rc = tile_order_step(r, F, cam, p, timed == 0 ? 0 : timed == 2 ? 1 : walk_decided ? 2 : walk_pending ? 3 : -1);
+        if (rc != RT_OK) return rc;
     }
     if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed], st));
     if (s->ext) kext::launch_frame(view, F, L);
@@ -900,6 +971,8 @@ int rt_renderer_destroy(rt_renderer *r) {
     if (r->d_rgb) (void)hipFree(r->d_rgb);
     if (r->d_pt) (void)hipFree(r->d_pt);
     if (r->d_samples) (void)hipFree(r->d_samples);
+    if (r->d_order) (void)hipFree(r->d_order);
+    if (r->d_cost) (void)hipFree(r->d_cost);
     for (auto &e : r->tev)
         if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(r->stream);

@@ -525,3 +525,34 @@ def test_lds_node_kernels_equal_global_kernel(rt, torch, monkeypatch, kind, spp,
         assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
     assert np.array_equal(rg.accumulator(), rl.accumulator())
     assert rg.counters() == rl.counters()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recipe,spp,mode,shards", [("teapotF", 1, 0, 1), ("mig16", 1, 0, 1), ("teapotF", 4, 0, 3),
+                                                    ("cfg3", 2, 1, 1)])
+def test_measured_tile_order_keeps_frames(rt, torch, monkeypatch, recipe, spp, mode, shards):
+    """The longest-tile-first dispatch order (costs recorded on the 3rd frame, applied from
+    the 4th) must not change any frame: 7 frames against RT_TILE_ORDER=0."""
+    W, H = 200, 120
+    monkeypatch.setenv("RT_TILE_ORDER", "0")
+    s_a = rt.Scene.recipe(recipe)
+    monkeypatch.setenv("RT_TILE_ORDER", "1")
+    s_b = rt.Scene.recipe(recipe)
+    ra, rb = rt.Renderer(s_a, W, H), rt.Renderer(s_b, W, H)
+    ra.mode = rb.mode = mode
+    depth = 1 if mode == 0 else 6
+    dev = torch.device("cuda", 0)
+    for f in range(7):
+        if shards == 1:
+            a, b = ra.tick_host(spp=spp, depth=depth, frame=f), rb.tick_host(spp=spp, depth=depth, frame=f)
+        else:
+            cap = ra.shard_capacity(shards)
+            ta = torch.zeros(cap, dtype=torch.int32, device=dev)
+            tb = torch.zeros(cap, dtype=torch.int32, device=dev)
+            ra.render_shard(ta, 1, shards, spp=spp, depth=depth, frame=f)
+            rb.render_shard(tb, 1, shards, spp=spp, depth=depth, frame=f)
+            torch.cuda.synchronize()
+            a, b = ta.cpu().numpy(), tb.cpu().numpy()
+        assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
+    assert np.array_equal(ra.accumulator(), rb.accumulator())
+    assert ra.counters() == rb.counters()

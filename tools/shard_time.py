@@ -26,12 +26,12 @@ def main():
     a = ap.parse_args()
     scene = rt.Scene.recipe(a.scene)
     out = {}
-    for n in (1, 2, 4, 8):
+    for n in (1, 2, 4, 8):   # 8 warm-up frames: walk timing + tile-order recording settle first
         r = rt.Renderer(scene, a.w, a.h)
         cap = r.shard_capacity(n)
         tiles = torch.zeros(cap, dtype=torch.int32, device="cuda")
         st = torch.cuda.Stream()
-        for f in range(3):
+        for f in range(8):
             r.render_shard(tiles, n - 1, n, spp=n, depth=a.depth, frame=f, stream=st.cuda_stream)
         torch.cuda.synchronize()
         c0 = r.counters()
@@ -39,7 +39,7 @@ def main():
         with torch.cuda.stream(st):
             ev[0].record()
             for f in range(a.frames):
-                r.render_shard(tiles, n - 1, n, spp=n, depth=a.depth, frame=3 + f, stream=st.cuda_stream)
+                r.render_shard(tiles, n - 1, n, spp=n, depth=a.depth, frame=8 + f, stream=st.cuda_stream)
             ev[1].record()
         torch.cuda.synchronize()
         c1 = r.counters()

@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=1)
     ap.add_argument("--depth", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--per-step-events", action="store_true", help="HIP event pair around every launch at N = 1 too")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline sample")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="HBM traffic per launch from rocprofv3 PMC passes (tools/pmc_summary.py)")
@@ -137,13 +138,22 @@ def main():
     drain()
     torch.cuda.synchronize(device)
     c0 = rend.counters()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events on the launch stream: at N = 1 one pair brackets the timed region (per-launch
+    # average = region / steps; no event packets between the frames), at N > 1 a pair around
+    # each shard render (the exchange runs between them)
+    per_step_events = world > 1 or args.per_step_events
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps if per_step_events else 1)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
+    if not per_step_events:
+        evs[0][0].record(stream)
     for k in range(args.steps):
-        step(args.warmup + k, evs[k])
+        step(args.warmup + k, evs[k] if per_step_events else None)
+    if not per_step_events:
+        evs[0][1].record(stream)
     drain()                                 # the last frame's gather + assembly are inside the timed region
     torch.cuda.synchronize(device)
     if dist:
@@ -151,7 +161,7 @@ def main():
     t1 = time.perf_counter()
     c1 = rend.counters()
     elapsed = t1 - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) / (1 if per_step_events else args.steps)
     primary = c1["primary"] - c0["primary"]
     shadow = c1["shadow"] - c0["shadow"]
     bounce = c1["bounce"] - c0["bounce"]

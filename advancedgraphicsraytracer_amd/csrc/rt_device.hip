@@ -33,9 +33,6 @@
 #include "rt_dev_types.h"
 #include "rt_internal.h"
 
-#ifndef RT_LDS_WG_TILES
-#define RT_LDS_WG_TILES 16   // must match rt_kernels.inc
-#endif
 
 
 // ====================================================================== host side
@@ -61,10 +58,10 @@ struct rt_scene {
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
     int walk = RT_WALK_LANE;    // camera-ray walk of the global-node primary+shadow kernel
     bool ext = false;           // needs the kext kernels (cubes, quads, textures, non-Light light)
+    bool pt_dynamic = true;         // wavefront levels >= 1 fetch chunks dynamically (RT_PT_DYNAMIC=0: static)
     bool pt_wavefront = true;   // depth >= 2 path tracing: wavefront (k_pt_level) vs one kernel (k_render)
     uint32_t pt_drain_level = 64;   // bounce level from which the wavefront always drains (64 = never forced)
     double pt_drain_rounds = 1.0;   // ... and it drains any level holding <= this many rounds of resident lanes
-    bool pt_full_grid = false;      // levels >= 1: one wave per queue slot group instead of a resident grid
     bool tile_order = true;         // measured-cost (longest first) tile order (RT_TILE_ORDER=0: off)
     uint32_t split_units = 20000;   // sample split below ~5 rounds of the 4096 resident waves
     uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per renderer: 12 GB of the 288 GB HBM
@@ -487,10 +484,10 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     }
     // RT_PT_WAVEFRONT=0 selects the one-kernel path tracer (k_render<path, MAXD>) for A/B runs
     if (const char *e = std::getenv("RT_PT_WAVEFRONT")) s->pt_wavefront = std::atoi(e) != 0;
+    if (const char *e = std::getenv("RT_PT_DYNAMIC")) s->pt_dynamic = std::atoi(e) != 0;
     // RT_PT_DRAIN_LEVEL / RT_PT_MEM_MB: wavefront drain level and path-state budget (A/B runs)
     if (const char *e = std::getenv("RT_PT_DRAIN_LEVEL")) s->pt_drain_level = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_DRAIN_ROUNDS")) s->pt_drain_rounds = std::max(0.0, std::atof(e));
-    if (const char *e = std::getenv("RT_PT_FULL_GRID")) s->pt_full_grid = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_TILE_ORDER")) s->tile_order = std::atoi(e) != 0;
     // RT_SPLIT_UNITS: sample-split target units (0 = never split)
     if (const char *e = std::getenv("RT_SPLIT_UNITS")) s->split_units = (uint32_t)std::max(0, std::atoi(e));
@@ -564,7 +561,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     // wave count is a multiple of kQueueSegs, so a segment never gets more than this
     const uint64_t seg_cap = ((np / 64u + kQueueSegs - 1) / kQueueSegs + 1) * 64u;
     const size_t qbytes = (size_t)seg_cap * kQueueSegs * 4u;
-    const size_t cbytes = (size_t)(F.depth + 1) * kQueueSegs * 64u;
+    const size_t cbytes = (size_t)(F.depth + 1) * (kQueueSegs + 8u) * 64u;   // queue counts + chunk heads
     const size_t need = (size_t)(np * (per_path - 8u) + 2 * qbytes + npix * 16u + cbytes + 4096u);
     if (need > r->pt_bytes) {
         if (r->d_pt) HIP_TRY(hipFree(r->d_pt));
@@ -583,6 +580,8 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     P.sum = reinterpret_cast<float4 *>(take(npix * 16u));
     P.qcount = reinterpret_cast<uint32_t *>(take(cbytes));
     P.seg_cap = (uint32_t)seg_cap;
+    P.qhead = P.qcount + (size_t)(F.depth + 1) * kQueueSegs * 16u;
+    P.dynamic = s->pt_dynamic ? 1 : 0;
     P.rec = reinterpret_cast<float4 *>(take((size_t)(F.depth - 1) * np * 32u));
     const size_t lds = stack_bytes(s);
     // levels are compacted level by level until one is small enough to drain (k_pt_level)
@@ -598,8 +597,8 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
             P.level = level;
             P.queue_in = (level & 1u) ? q1 : q0;
             P.queue_out = (level & 1u) ? q0 : q1;
-            const int resident = s->ext ? kext::launch_pt_level(view, F, P, tex, s->pt_full_grid, lds, s->num_cus, st)
-                                        : kcore::launch_pt_level(view, F, P, tex, s->pt_full_grid, lds, s->num_cus, st);
+            const int resident = s->ext ? kext::launch_pt_level(view, F, P, tex, lds, s->num_cus, st)
+                                        : kcore::launch_pt_level(view, F, P, tex, lds, s->num_cus, st);
             if (level >= drain_level) break;           // that launch finished every remaining level
             P.drain_below = (uint32_t)std::min<double>(4e9, s->pt_drain_rounds * resident);
         }
@@ -730,7 +729,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     dim3 grid, block;
     size_t lds;
     if (lds_kind == 64) {
-        grid = dim3((F.nunits + RT_LDS_WG_TILES - 1) / RT_LDS_WG_TILES);
+        grid = dim3((F.nunits + 15) / 16);
         block = dim3(1024);
         lds = lds_scene_bytes(s);
     } else if (lds_kind == 48) {

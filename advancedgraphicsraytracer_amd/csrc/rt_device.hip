@@ -635,6 +635,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
         r->order_key = key;
         r->order_state = 0;
         if (n != r->order_n) {
+            HIP_TRY(hipDeviceSynchronize());                             // frames may still read them
             if (r->d_order) HIP_TRY(hipFree(r->d_order));
             if (r->d_cost) HIP_TRY(hipFree(r->d_cost));
             r->d_order = r->d_cost = nullptr;
@@ -655,6 +656,10 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
         use = 0;
     }
     if (use >= 0) {
+        // once per parameter set: a device-wide sync orders the cost read after the recording
+        // frame and the order write after every frame still reading the previous order,
+        // whatever streams the caller used
+        HIP_TRY(hipDeviceSynchronize());
         std::vector<uint32_t> cost(n), ord(n);
         HIP_TRY(hipMemcpy(cost.data(), r->d_cost + (size_t)use * n, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
         for (uint32_t i = 0; i < n; ++i) ord[i] = i;

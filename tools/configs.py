@@ -65,7 +65,7 @@ def run(cfg, frames, warmup):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=5)   # walk timing + tile-order recording settle in 4 frames
     ap.add_argument("--only", default="")
     ap.add_argument("--json", default="")
     ap.add_argument("--custom", action="append", default=[], help="scene,w,h,spp,depth (repeatable)")

@@ -5,7 +5,7 @@ Each config is one Renderer::Tick equivalent (rt_render_frame) per frame on a de
 stream; frames are timed with HIP events around the launch, rays come from the library's
 counters (primary + shadow + bounce = closest-hit + any-hit rays actually traced).
 
-usage: configs.py [--frames 20] [--warmup 3] [--only cfg3,cfg5] [--json out.json]
+usage: configs.py [--frames 20] [--warmup 5] [--only cfg3,cfg5] [--json out.json]
 """
 import argparse
 import json

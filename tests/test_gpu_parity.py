@@ -439,6 +439,7 @@ def test_frame_kernel_name(rt):
     ("cfg3", 136, 80, 4, 4, {"RT_PT_MEM_MB": "1"}),             # 1 MB of path state: one sample per batch
     ("cfg5", 96, 64, 3, 10, {"RT_PT_MEM_MB": "2"}),             # uneven batches
     ("teapotF", 72, 40, 2, 2, {}),                              # depth 2: a single continuation level
+    ("cfg3", 64, 48, 2, 32, {}),                                # the deepest Trace (32): meta bits, records
 ])
 def test_wavefront_equals_one_kernel_path_tracer(rt, torch, monkeypatch, recipe, W, H, spp, depth, env):
     """The wavefront path tracer (k_pt_level + k_pt_finish: compaction between bounce
@@ -556,3 +557,19 @@ def test_measured_tile_order_keeps_frames(rt, torch, monkeypatch, recipe, spp, m
         assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
     assert np.array_equal(ra.accumulator(), rb.accumulator())
     assert ra.counters() == rb.counters()
+
+
+# ---- BASELINE.json configs at their full size against the oracle
+@pytest.mark.parametrize("recipe,W,H,spp,depth,frames", [
+    ("teapotF", 3840, 2160, 1, 1, 5),     # 4K, past the walk timing and the tile-order switch (frame 4)
+    ("cfg3", 1920, 1080, 4, 4, 1),        # config 3: Shiba Dielectric + glider Mirror, 4 spp, depth 4
+    ("cfg5", 1920, 1080, 16, 10, 1),      # config 5: 16 spp path trace, depth 10 (wavefront, one batch)
+    ("mig16", 1920, 1080, 1, 1, 5),       # config 4 on one GPU
+])
+def test_baseline_configs_full_size(rt, scenes, recipe, W, H, spp, depth, frames):
+    g, o = scenes(recipe)
+    got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, W, H, spp, depth, frames=frames)
+    assert np.array_equal(got, want), f"{(got != want).sum()} RGB8 mismatches"
+    assert np.abs(gacc - acc).max() <= PIX_TOL
+    assert c["shadow"] == st["shadow"]
+    assert c["bounce"] == st["isect"] - W * H * spp * frames

@@ -103,7 +103,7 @@ struct PathArgs {
     uint32_t s0, batch_spp, npaths, level;
     uint32_t seg_cap;                    // entries per queue segment
     int dynamic;                         // levels >= 1 take their chunks from the qhead counters
-    uint32_t *qhead;                     // [level][8] chunk head counters, 64 B apart
+    uint32_t *qhead;                     // [level][kQueueSegs] head counters, 64 B apart (k_pt_level uses 8)
     uint32_t drain_level, drain_below;   // drain (run every remaining level) from this level on /
                                          // at any level holding at most this many paths
     float4 *state;
@@ -128,6 +128,8 @@ struct PathArgs {
                                  uint32_t n, hipStream_t st);                                     \
     int launch_pt_level(const SceneView &S, const FrameArgs &F, const PathArgs &P, bool tex,      \
                         size_t lds, uint32_t num_cus, hipStream_t st);                            \
+    void launch_pt_lanes(const SceneView &S, const FrameArgs &F, const PathArgs &P, bool tex,     \
+                         size_t lds, uint32_t num_cus, hipStream_t st);                           \
     void launch_pt_finish(const FrameArgs &F, const PathArgs &P, bool last, hipStream_t st);      \
     }
 RT_DECLARE_LAUNCHERS(kcore)

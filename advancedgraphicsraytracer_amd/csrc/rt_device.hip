@@ -58,6 +58,7 @@ struct rt_scene {
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
     int walk = RT_WALK_LANE;    // camera-ray walk of the global-node primary+shadow kernel
     bool ext = false;           // needs the kext kernels (cubes, quads, textures, non-Light light)
+    bool pt_lanes = true;           // levels >= 1 run the lane state machine (RT_PT_LANES=0: k_pt_level)
     bool pt_dynamic = true;         // wavefront levels >= 1 fetch chunks dynamically (RT_PT_DYNAMIC=0: static)
     bool pt_wavefront = true;   // depth >= 2 path tracing: wavefront (k_pt_level) vs one kernel (k_render)
     uint32_t pt_drain_level = 64;   // bounce level from which the wavefront always drains (64 = never forced)
@@ -485,6 +486,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     // RT_PT_WAVEFRONT=0 selects the one-kernel path tracer (k_render<path, MAXD>) for A/B runs
     if (const char *e = std::getenv("RT_PT_WAVEFRONT")) s->pt_wavefront = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_DYNAMIC")) s->pt_dynamic = std::atoi(e) != 0;
+    if (const char *e = std::getenv("RT_PT_LANES")) s->pt_lanes = std::atoi(e) != 0;
     // RT_PT_DRAIN_LEVEL / RT_PT_MEM_MB: wavefront drain level and path-state budget (A/B runs)
     if (const char *e = std::getenv("RT_PT_DRAIN_LEVEL")) s->pt_drain_level = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_DRAIN_ROUNDS")) s->pt_drain_rounds = std::max(0.0, std::atof(e));
@@ -561,7 +563,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     // wave count is a multiple of kQueueSegs, so a segment never gets more than this
     const uint64_t seg_cap = ((np / 64u + kQueueSegs - 1) / kQueueSegs + 1) * 64u;
     const size_t qbytes = (size_t)seg_cap * kQueueSegs * 4u;
-    const size_t cbytes = (size_t)(F.depth + 1) * (kQueueSegs + 8u) * 64u;   // queue counts + chunk heads
+    const size_t cbytes = (size_t)(F.depth + 1) * (2u * kQueueSegs) * 64u;   // queue counts + head counters
     const size_t need = (size_t)(np * (per_path - 8u) + 2 * qbytes + npix * 16u + cbytes + 4096u);
     if (need > r->pt_bytes) {
         if (r->d_pt) HIP_TRY(hipFree(r->d_pt));
@@ -597,10 +599,16 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
             P.level = level;
             P.queue_in = (level & 1u) ? q1 : q0;
             P.queue_out = (level & 1u) ? q0 : q1;
-            const int resident = s->ext ? kext::launch_pt_level(view, F, P, tex, lds, s->num_cus, st)
-                                        : kcore::launch_pt_level(view, F, P, tex, lds, s->num_cus, st);
+            int resident = 0;
+            if (level > 0 && s->pt_lanes) {             // incoherent levels: the lane state machine
+                if (s->ext) kext::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, st);
+                else kcore::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, st);
+            } else {
+                resident = s->ext ? kext::launch_pt_level(view, F, P, tex, lds, s->num_cus, st)
+                                  : kcore::launch_pt_level(view, F, P, tex, lds, s->num_cus, st);
+            }
             if (level >= drain_level) break;           // that launch finished every remaining level
-            P.drain_below = (uint32_t)std::min<double>(4e9, s->pt_drain_rounds * resident);
+            if (level == 0) P.drain_below = (uint32_t)std::min<double>(4e9, s->pt_drain_rounds * resident);
         }
         const bool last = s0 + P.batch_spp >= F.spp;
         if (s->ext) kext::launch_pt_finish(F, P, last, st);

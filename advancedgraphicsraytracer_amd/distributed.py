@@ -3,9 +3,9 @@
 One process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm).  Every rank
 holds a full replica of the scene (<= 11 MB for the largest benchmark scene) and renders
 the 8x8 tiles t with t % world == rank into a packed buffer; the frame's single
-collective is an all-gather of those packed buffers (xGMI point-to-point links carry
-1/world of the RGB8 frame each), after which rank 0 unshuffles them into the row-major
-image.  Nothing else crosses ranks: pixels are independent in the reference's Tick
+collective gathers those packed buffers to rank 0 (each rank's xGMI link to rank 0 carries
+1/world of the RGB8 frame; SURVEY.md 5: gather-to-root, not a ring), after which rank 0
+unshuffles them into the row-major image.  Nothing else crosses ranks: pixels are independent in the reference's Tick
 (renderer.cpp:215-244).
 """
 import torch
@@ -13,14 +13,22 @@ import torch.distributed as dist
 
 
 def gather_into(gathered, tiles, group=None, async_op=False):
-    """all_gather of equal-size packed tile buffers into one flat tensor [world * cap].
-    With async_op the work handle is returned (wait() orders the caller's current stream
-    after the collective, as ProcessGroupNCCL does)."""
+    """Gather of equal-size packed tile buffers to rank 0, into one flat tensor [world * cap]
+    there (other ranks only send: 1/world of the frame each over its xGMI link to rank 0,
+    instead of the world-fold traffic of an all-gather).  With async_op the work handle is
+    returned (wait() orders the caller's current stream after the collective, as
+    ProcessGroupNCCL does).  Backends without gather fall back to an all-gather."""
+    rank = dist.get_rank(group)
+    dst = dist.get_global_rank(group, 0) if group is not None else 0
+    parts = list(gathered.view(-1, tiles.numel()).unbind(0)) if rank == 0 else None
     try:
-        return dist.all_gather_into_tensor(gathered, tiles, group=group, async_op=async_op)
-    except (RuntimeError, NotImplementedError, AttributeError, ValueError):   # backends without the fused form
-        parts = list(gathered.view(-1, tiles.numel()).unbind(0))
-        return dist.all_gather(parts, tiles, group=group, async_op=async_op)
+        return dist.gather(tiles, gather_list=parts, dst=dst, group=group, async_op=async_op)
+    except (RuntimeError, NotImplementedError, AttributeError, ValueError):
+        try:
+            return dist.all_gather_into_tensor(gathered, tiles, group=group, async_op=async_op)
+        except (RuntimeError, NotImplementedError, AttributeError, ValueError):
+            parts = list(gathered.view(-1, tiles.numel()).unbind(0))
+            return dist.all_gather(parts, tiles, group=group, async_op=async_op)
 
 
 class ShardedFrame:

@@ -9,8 +9,8 @@ timing; synthetic data = the bundled teapot mesh + the synthetic constant sky.
 
 N > 1 (python -m torch.distributed.run ... bench.py --gpus N): weak scaling -- the
 frame's 8x8 tiles are interleaved over the ranks and the frame is rendered at spp = N,
-so every GPU traces one 1080p frame's worth of samples per step; one RCCL all-gather of
-the packed RGB8 tiles per frame assembles the image on rank 0.  The
+so every GPU traces one 1080p frame's worth of samples per step; one RCCL gather of
+the packed RGB8 tiles to rank 0 per frame assembles the image there.  The
 gather of frame i runs while frame i+1 renders (double-buffered tiles); the timed region
 ends after the last frame's gather and assembly.
 value = all rays traced by all ranks / max-over-ranks wall time.

@@ -20,7 +20,7 @@ for s in "$@"; do
         smoke) step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
         tests) step gpu_tests 300 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
         bench) step bench 600 python bench.py --steps 30 --warmup 5 ;;
-        prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+        prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 100 --warmup 5 --no-cpu-baseline ;;
         pmc)
             step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o pmc -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
             step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o pmc -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline

@@ -20,8 +20,13 @@ HEADERS = ["rt_math.h", "rt_internal.h", "rt_libm.h", "rt_dev_types.h", "rt_kern
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off + IEEE div/sqrt (hipcc's default) keep the kernels' float results
 # bit-identical to the reference's evaluation order.
+# -fno-slp-vectorize: plain -O3 packs adjacent f32 adds/multiplies into v_pk_*_f32 plus the
+# v_mov shuffles feeding them; scalar f32 issues faster on gfx950 and the frame kernel drops
+# from 91 to 68 VGPRs (5 -> 7 waves/SIMD): TEAPOT-F 1080p 0.120 -> 0.106 ms, CFG5-sub 10.4 ->
+# 9.4 ms, bit-identical (profiles/r01/ab_nslp_*.json).
 LIBS = ["-lz"]   # zlib: PNG textures (rt_image_load)
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC",
+         "-shared",
          "-Wall", "-Wno-unused-function"]
 
 

@@ -71,7 +71,15 @@ RT_HD uint32_t wang_hash(uint32_t s) {
     s = s ^ (s >> 15);
     return s;
 }
-RT_HD uint32_t init_seed(uint32_t base) { return wang_hash((base + 1u) * 17u); }
+// InitSeed(base) = WangHash((base + 1) * 17) is a bijection, so exactly one base (1768515948)
+// maps to 0, a fixed point of xorshift32: every draw would be 0 and the rejection loops of
+// randomInUnitDisk / GetRandomPoint would never end.  With per-pixel seeds that base is
+// reached (1080p spp 1: frame 852, pixel (108, 942)), so a zero seed is replaced by the
+// reference's global start seed 0x12345678 (template/template.cpp:673); the oracle does the same.
+RT_HD uint32_t init_seed(uint32_t base) {
+    const uint32_t h = wang_hash((base + 1u) * 17u);
+    return h ? h : 0x12345678u;
+}
 RT_HD uint32_t rnd_u(uint32_t &s) { s ^= s << 13; s ^= s >> 17; s ^= s << 5; return s; }
 RT_HD float rnd_f(uint32_t &s) { return (float)rnd_u(s) * 2.3283064365387e-10f; }
 

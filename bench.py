@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=1)
     ap.add_argument("--depth", type=int, default=1)
+    ap.add_argument("--ramp-seconds", type=float, default=0.5,
+                    help="untimed frames before the warm-up steps until this much wall time has passed: the "
+                         "GPU clocks ramp up over ~0.1 s, and 5 warm-up frames are only ~0.5 ms of work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--per-step-events", action="store_true", help="HIP event pair around every launch at N = 1 too")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline sample")
@@ -133,8 +136,26 @@ def main():
             with torch.cuda.stream(stream):
                 sharded.flush(stream=sptr)
 
+    # clock ramp (untimed, before the W warm-up steps): blocks of 20 frames until
+    # --ramp-seconds have passed; at N > 1 the ranks agree on every block (the per-frame
+    # gather is a collective, so every rank must submit the same frames)
+    nf = 0
+    t_ramp = time.perf_counter()
+    while args.ramp_seconds > 0:
+        for _ in range(20):
+            step(nf)
+            nf += 1
+        drain()
+        torch.cuda.synchronize(device)
+        more = torch.tensor([1 if time.perf_counter() - t_ramp < args.ramp_seconds else 0], device=f"cuda:{device}")
+        if dist:
+            dist.all_reduce(more, op=dist.ReduceOp.MIN)
+        if not more.item():
+            break
+    ramp_frames = nf
     for i in range(args.warmup):
-        step(i)
+        step(nf)
+        nf += 1
     drain()
     torch.cuda.synchronize(device)
     c0 = rend.counters()
@@ -151,7 +172,7 @@ def main():
     if not per_step_events:
         evs[0][0].record(stream)
     for k in range(args.steps):
-        step(args.warmup + k, evs[k] if per_step_events else None)
+        step(nf + k, evs[k] if per_step_events else None)
     if not per_step_events:
         evs[0][1].record(stream)
     drain()                                 # the last frame's gather + assembly are inside the timed region
@@ -204,6 +225,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "clock_ramp_frames": ramp_frames,
             "ms_per_step": round(wall / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",

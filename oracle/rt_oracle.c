@@ -164,7 +164,13 @@ static uint32_t wang_hash(uint32_t s) {
     s = s ^ (s >> 15);
     return s;
 }
-uint32_t or_init_seed(uint32_t base) { return wang_hash((base + 1u) * 17u); }
+/* per-pixel seeds: InitSeed (template/template.cpp:697-704); the single base whose WangHash is
+ * 0 (a fixed point of xorshift32: the rejection loops would never end) gets the reference's
+ * global start seed 0x12345678 (template/template.cpp:673) -- as rt_math.h init_seed */
+uint32_t or_init_seed(uint32_t base) {
+    const uint32_t h = wang_hash((base + 1u) * 17u);
+    return h ? h : 0x12345678u;
+}
 static inline uint32_t rnd_u(uint32_t *s) { uint32_t x = *s; x ^= x << 13; x ^= x >> 17; x ^= x << 5; *s = x; return x; }
 static inline float rnd_f(uint32_t *s) { return (float)rnd_u(s) * 2.3283064365387e-10f; }
 

@@ -575,3 +575,22 @@ def test_baseline_configs_full_size(rt, scenes, recipe, W, H, spp, depth, frames
     assert np.abs(gacc - acc).max() <= PIX_TOL
     assert c["shadow"] == st["shadow"]
     assert c["bounce"] == st["isect"] - W * H * spp * frames
+
+
+# InitSeed maps exactly one base to 0, a fixed point of xorshift32 (every draw 0: the camera
+# lens and light-point rejection loops would never end); both sides substitute 0x12345678.
+ZERO_SEED_BASE = 1768515948
+
+
+@pytest.mark.parametrize("depth,spp", [(1, 1), (4, 1), (3, 2)])
+def test_zero_seed_pixel_terminates_and_matches(rt, scenes, depth, spp):
+    g, o = scenes("teapotF")
+    W, H = 160, 96
+    frame = ZERO_SEED_BASE // (W * H * spp)          # the frame whose seed range holds the base
+    r = rt.Renderer(g, W, H)
+    got = r.tick_host(spp=spp, depth=depth, frame=frame)
+    acc = np.zeros((W * H, 4), np.float32)
+    want, st = o.tick(W, H, acc, spp=spp, depth=depth, frame=frame)
+    assert np.abs(r.accumulator() - acc).max() <= PIX_TOL
+    assert np.array_equal(got, want)
+    assert r.counters()["shadow"] == st["shadow"]

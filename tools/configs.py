@@ -30,13 +30,20 @@ CONFIGS = {
 }
 
 
-def run(cfg, frames, warmup):
+def run(cfg, frames, warmup, ramp_s=0.5):
     scene = rt.Scene.recipe(cfg["scene"], device=0)
     r = rt.Renderer(scene, cfg["w"], cfg["h"])
     out = torch.zeros(cfg["w"] * cfg["h"], dtype=torch.int32, device="cuda:0")
     st = torch.cuda.Stream()
+    nf, t_ramp = 0, time.perf_counter()
+    while time.perf_counter() - t_ramp < ramp_s:     # GPU clock ramp (untimed), as bench.py
+        for _ in range(4):
+            r.Tick(out, spp=cfg["spp"], depth=cfg["depth"], frame=nf, stream=st.cuda_stream)
+            nf += 1
+        torch.cuda.synchronize()
     for i in range(warmup):
-        r.Tick(out, spp=cfg["spp"], depth=cfg["depth"], frame=i, stream=st.cuda_stream)
+        r.Tick(out, spp=cfg["spp"], depth=cfg["depth"], frame=nf, stream=st.cuda_stream)
+        nf += 1
     torch.cuda.synchronize()
     c0 = r.counters()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(frames)]
@@ -44,7 +51,7 @@ def run(cfg, frames, warmup):
     with torch.cuda.stream(st):
         for k in range(frames):
             ev[k][0].record(st)
-            r.Tick(out, spp=cfg["spp"], depth=cfg["depth"], frame=warmup + k, stream=st.cuda_stream)
+            r.Tick(out, spp=cfg["spp"], depth=cfg["depth"], frame=nf + k, stream=st.cuda_stream)
             ev[k][1].record(st)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0

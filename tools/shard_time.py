@@ -2,11 +2,12 @@
 """Per-rank frame time of bench.py's N > 1 workload, measured on one GPU: the 1/N screen
 shard at spp = N (weak scaling), render + (rank-0) assembly, for N = 1, 2, 4, 8.
 Predicts the driver's scaling efficiency up to the gather.
-usage: shard_time.py [--scene teapotF] [--depth 1] [--frames 30] [--split-units U]"""
+usage: shard_time.py [--scene teapotF] [--depth 1] [--frames 30]   (RT_SPLIT_UNITS=U: split threshold)"""
 import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -26,6 +27,16 @@ def main():
     a = ap.parse_args()
     scene = rt.Scene.recipe(a.scene)
     out = {}
+    r0 = rt.Renderer(scene, a.w, a.h)                  # GPU clock ramp (untimed), as bench.py
+    o0 = torch.zeros(a.w * a.h, dtype=torch.int32, device="cuda")
+    t0, f = time.perf_counter(), 0
+    while time.perf_counter() - t0 < 0.5:
+        r0.Tick(o0, spp=1, depth=a.depth, frame=f)
+        f += 1
+        if f % 20 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    r0.close()
     for n in (1, 2, 4, 8):   # 8 warm-up frames: walk timing + tile-order recording settle first
         r = rt.Renderer(scene, a.w, a.h)
         cap = r.shard_capacity(n)

@@ -65,6 +65,8 @@ struct rt_scene {
     double pt_drain_rounds = 1.0;   // ... and it drains any level holding <= this many rounds of resident lanes
     bool tile_order = true;         // measured-cost (longest first) tile order (RT_TILE_ORDER=0: off)
     uint32_t split_units = 20000;   // sample split below ~5 rounds of the 4096 resident waves
+    int32_t heavy_split = -1;       // primary+shadow frames: the costliest tiles run as two half-tile
+                                    // waves (RT_SPLIT_HEAVY = count; -1: ntiles / 32)
     uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per renderer: 12 GB of the 288 GB HBM
                                               // holds all 16 spp of a 1080p depth-10 frame
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
@@ -90,6 +92,11 @@ struct rt_renderer {
     uint32_t order_n = 0;
     uint64_t order_key = 0;
     int order_state = 0;        // 0 idle, 1 costs recorded, 2 order active
+    uint32_t order_split = 0;   // leading tiles of the split order that run as two half-tile units
+    int split_phase = -1;       // -1 decided / not tried; 0..3 timing frames (plain, split, plain, split)
+    bool use_split = false;     // the split order measured faster
+    hipEvent_t sev[8] = {};     // split timing: events 2i, 2i+1 around timing frame i
+    float split_ms[4] = {};
     int tune = 0;
     bool wave = false;
     hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -493,6 +500,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_TILE_ORDER")) s->tile_order = std::atoi(e) != 0;
     // RT_SPLIT_UNITS: sample-split target units (0 = never split)
     if (const char *e = std::getenv("RT_SPLIT_UNITS")) s->split_units = (uint32_t)std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("RT_SPLIT_HEAVY")) s->heavy_split = std::max(-1, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
@@ -628,7 +636,9 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
 // the 4th frame); otherwise frame 1 records and frame 2 applies.  Pixel values do not depend
 // on the order.  walk_phase: -1 no walk timing pending, 0 / 1 this frame times the lane /
 // wave walk, 2 the walk was picked on this frame, 3 the timing has not started yet.
-int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt_frame_params *p, int walk_phase) {
+int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt_frame_params *p, int walk_phase,
+                    bool split_ok, int &split_timed) {
+    split_timed = -1;
     uint64_t key = 1469598103934665603ull;
     auto mix = [&](const void *d, size_t n) {
         const unsigned char *c = static_cast<const unsigned char *>(d);
@@ -648,7 +658,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
             if (r->d_cost) HIP_TRY(hipFree(r->d_cost));
             r->d_order = r->d_cost = nullptr;
             r->order_n = 0;
-            HIP_TRY(hipMalloc(&r->d_order, n * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&r->d_order, 3u * n * sizeof(uint32_t)));   // plain order | split order
             HIP_TRY(hipMalloc(&r->d_cost, 2u * n * sizeof(uint32_t)));   // one cost map per camera walk
             r->order_n = n;
         }
@@ -672,10 +682,45 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
         HIP_TRY(hipMemcpy(cost.data(), r->d_cost + (size_t)use * n, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
         for (uint32_t i = 0; i < n; ++i) ord[i] = i;
         std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
-        HIP_TRY(hipMemcpy(r->d_order, ord.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+        // The costliest tiles can bound the frame's tail (one wave's latency chain): the split
+        // order runs the first k of them as two waves of half a tile each (entry bit 31 =
+        // split, bit 30 = which half).  It shortens tail-bound frames (mig29 x16 -10 %, 720p
+        // TEAPOT-F -9 %) and lengthens throughput-bound ones (1080p TEAPOT-F +9 %: the half-
+        // empty waves cost issue slots), so with RT_SPLIT_HEAVY = -1 (default) both orders are
+        // timed on two frames each and the faster one is kept; frames are identical either way.
+        uint32_t k = 0;
+        if (split_ok) {
+            const int32_t hs = r->scene->heavy_split;
+            k = std::min<uint32_t>(n, hs < 0 ? n / 32u : (uint32_t)hs);
+        }
+        std::vector<uint32_t> ent(ord);
+        for (uint32_t i = 0; i < k; ++i) {
+            ent.push_back(ord[i] | 0x80000000u);
+            ent.push_back(ord[i] | 0xC0000000u);
+        }
+        for (uint32_t i = k; i < n; ++i) ent.push_back(ord[i]);
+        HIP_TRY(hipMemcpy(r->d_order, ent.data(), ent.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        r->order_split = k;
         r->order_state = 2;
+        r->use_split = k > 0 && r->scene->heavy_split > 0;            // a forced count: no timing
+        r->split_phase = (k > 0 && r->scene->heavy_split < 0) ? 0 : -1;
+        if (r->split_phase == 0 && !r->sev[0])
+            for (auto &e : r->sev) HIP_TRY(hipEventCreate(&e));
     }
-    if (r->order_state == 2) F.order = r->d_order;
+    if (r->order_state == 2) {
+        bool split = r->use_split;
+        if (r->split_phase == 4) {                                     // decide after the 4 timed frames
+            HIP_TRY(hipEventSynchronize(r->sev[7]));
+            for (int i = 0; i < 4; ++i) HIP_TRY(hipEventElapsedTime(&r->split_ms[i], r->sev[2 * i], r->sev[2 * i + 1]));
+            r->use_split = split = r->split_ms[1] + r->split_ms[3] < r->split_ms[0] + r->split_ms[2];
+            r->split_phase = -1;
+        } else if (r->split_phase >= 0) {
+            split = r->split_phase & 1;
+            split_timed = r->split_phase++;
+        }
+        F.order = split ? r->d_order + n : r->d_order;
+        F.nunits = F.ntiles_local * F.nchunks + (split ? r->order_split : 0u);   // split only with nchunks 1
+    }
     return RT_OK;
 }
 
@@ -789,15 +834,22 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
             if (r->tune == 4) view.wave_primary = r->wave ? 1 : 0;
         }
     }
+    int split_timed = -1;   // sev pair recorded around this launch
     if (s->tile_order) {
-        const int rc = tile_order_step(r, F, cam, p, timed == 0 ? 0 : timed == 2 ? 1 : walk_decided ? 2 : walk_pending ? 3 : -1);
+        // half-tile units: primary+shadow frames of the global-node kernel, whole-tile units only
+        const bool split_ok = mode == RT_MODE_PATH && md == 1 && lds_kind == 0 && F.nchunks <= 1;
+        const int rc = tile_order_step(r, F, cam, p, timed == 0 ? 0 : timed == 2 ? 1 : walk_decided ? 2 : walk_pending ? 3 : -1,
+                                       split_ok, split_timed);
         if (rc != RT_OK) return rc;
+        if (lds_kind == 0) L.grid = dim3((F.nunits + 3) / 4);
     }
     if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed], st));
+    if (split_timed >= 0) HIP_TRY(hipEventRecord(r->sev[2 * split_timed], st));
     if (s->ext) kext::launch_frame(view, F, L);
     else kcore::launch_frame(view, F, L);
     HIP_TRY(hipGetLastError());
     if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed + 1], st));
+    if (split_timed >= 0) HIP_TRY(hipEventRecord(r->sev[2 * split_timed + 1], st));
     if (F.nchunks > 1) {   // the pixels' samples in sample order, running average, RGB8
         PathArgs P{};
         P.batch_spp = p->spp;
@@ -986,6 +1038,8 @@ int rt_renderer_destroy(rt_renderer *r) {
     if (r->d_order) (void)hipFree(r->d_order);
     if (r->d_cost) (void)hipFree(r->d_cost);
     for (auto &e : r->tev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto &e : r->sev)
         if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(r->stream);
     delete r;

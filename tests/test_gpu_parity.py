@@ -533,19 +533,23 @@ def test_lds_node_kernels_equal_global_kernel(rt, torch, monkeypatch, kind, spp,
 @pytest.mark.gpu
 @pytest.mark.parametrize("recipe,spp,mode,shards", [("teapotF", 1, 0, 1), ("mig16", 1, 0, 1), ("teapotF", 4, 0, 3),
                                                     ("cfg3", 2, 1, 1)])
-def test_measured_tile_order_keeps_frames(rt, torch, monkeypatch, recipe, spp, mode, shards):
+@pytest.mark.parametrize("heavy", ["-1", "64"])
+def test_measured_tile_order_keeps_frames(rt, torch, monkeypatch, recipe, spp, mode, shards, heavy):
     """The longest-tile-first dispatch order (costs recorded on the 3rd frame, applied from
-    the 4th) must not change any frame: 7 frames against RT_TILE_ORDER=0."""
+    the 4th; primary+shadow frames then time the half-tile split order against the plain one
+    on 4 frames, or force it with RT_SPLIT_HEAVY=64) must not change any frame: 12 frames
+    against RT_TILE_ORDER=0."""
     W, H = 200, 120
     monkeypatch.setenv("RT_TILE_ORDER", "0")
     s_a = rt.Scene.recipe(recipe)
     monkeypatch.setenv("RT_TILE_ORDER", "1")
+    monkeypatch.setenv("RT_SPLIT_HEAVY", heavy)
     s_b = rt.Scene.recipe(recipe)
     ra, rb = rt.Renderer(s_a, W, H), rt.Renderer(s_b, W, H)
     ra.mode = rb.mode = mode
     depth = 1 if mode == 0 else 6
     dev = torch.device("cuda", 0)
-    for f in range(7):
+    for f in range(12):
         if shards == 1:
             a, b = ra.tick_host(spp=spp, depth=depth, frame=f), rb.tick_host(spp=spp, depth=depth, frame=f)
         else:

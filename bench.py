@@ -200,13 +200,14 @@ def main():
         if bp is not None and args.depth == 1:
             per_launch = (primary * bp + shadow * bs) / args.steps     # this rank's launch
             achieved = per_launch / (kern_ms * 1e-3) / 1e9
-            traffic = None
+            traffic = valu = None
             try:
                 with open(args.pmc_json) as f:
                     pmc = json.load(f)
                 key = f"{args.scene}_{W}x{H}_spp{spp}_d{args.depth}"
                 if key in pmc:
                     traffic = pmc[key]["hbm_bytes_per_launch"]
+                    valu = pmc[key].get("valu_insts_per_launch")
             except (OSError, ValueError, KeyError):
                 traffic = None
             roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -217,7 +218,10 @@ def main():
                         # ~0.1 MB): frac > 1 means "beyond the HBM roofline"; the HBM bytes the
                         # PMC counters see per launch, and their rate, are these
                         "hbm_measured_gbs": round(traffic / (kern_ms * 1e-3) / 1e9, 2) if traffic else None,
-                        "hbm_measured_frac": round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if traffic else None}
+                        "hbm_measured_frac": round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if traffic else None,
+                        # the binding resource: vector issue.  SQ_INSTS_VALU per launch (PMC pass) x 2
+                        # cycles per wave64 instruction over 1,024 SIMDs x the launch's cycles at 2.4 GHz
+                        "valu_issue_frac": round(valu * 2 / (1024 * kern_ms * 1e-3 * 2.4e9), 4) if valu else None}
         line = {
             "metric": "Mrays/s (primary+shadow) at 1080p",
             "value": round(tot_rays / wall / 1e6, 3),

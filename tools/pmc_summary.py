@@ -4,7 +4,7 @@ per k_render launch, applying MI355X_MICROARCH.md's gfx950 corrections: counters
 KB (x1024); FETCH_SIZE reports half of the bytes of a wide coalesced read, so it is
 doubled; WRITE_SIZE is exact for 16-B-per-lane stores.
 
-usage: pmc_summary.py KEY FETCH_DIR WRITE_DIR [OUT_JSON] [KERNEL_SUBSTR]
+usage: pmc_summary.py KEY FETCH_DIR WRITE_DIR [OUT_JSON] [KERNEL_SUBSTR] [VALU_DIR]
 """
 import csv
 import glob
@@ -35,6 +35,11 @@ def main():
            "hbm_read_bytes_per_launch": 2 * fetch_kb * 1024, "hbm_write_bytes_per_launch": write_kb * 1024,
            "hbm_bytes_per_launch": 2 * fetch_kb * 1024 + write_kb * 1024,
            "correction": "FETCH_SIZE x2 (gfx950 half-count on wide reads), KB x1024"}
+    vdir = sys.argv[6] if len(sys.argv) > 6 else os.path.join(os.path.dirname(fdir), "pmc_valu")
+    try:   # the VALU pass (SQ_INSTS_VALU: wave64 vector instructions per launch), if it was run
+        rec["valu_insts_per_launch"], _ = counter_means(vdir, "SQ_INSTS_VALU", kern)
+    except SystemExit:
+        pass
     data = {}
     if os.path.exists(out):
         with open(out) as fh:

@@ -131,6 +131,8 @@ int material_flag(const rt_material &m, float diffuse, float specular) {   // ge
     }
 }
 
+constexpr uint32_t kMaxNodes = 1u << 24;   // the packed word's leftFirst field is 24 bits wide
+
 int validate_bvh(const Bvh &b, uint32_t n) {
     if (b.nodes_used < 2 || b.nodes_used > b.nodes.size()) return fail(RT_ERR_INVALID, "BVH node count out of range");
     std::vector<uint8_t> seen(n, 0);
@@ -229,6 +231,10 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         if (!w || !h || (w & (w - 1)) || (h & (h - 1)))
             return fail(RT_ERR_INVALID, "sky texture must have power-of-two sides (renderer.h:18)");
     }
+    // interior nodes store a node index in the 24-bit leftFirst field of the packed device
+    // word (leftFirst << 8 | count): trees with more than 2^24 nodes cannot be addressed
+    if (d->bvh_nodes && d->bvh_num_nodes > kMaxNodes)
+        return fail(RT_ERR_UNSUPPORTED, "prebuilt BVH with more than 2^24 nodes (24-bit child index)");
     int rc = ensure_device(d->device);
     if (rc != RT_OK) return rc;
 
@@ -263,6 +269,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         delete s;
         return rc;
     }
+    if (s->bvh.nodes_used > kMaxNodes) { delete s; return fail(RT_ERR_UNSUPPORTED, "BVH with more than 2^24 nodes (24-bit child index)"); }
     if (s->bvh.max_leaf > 255) { delete s; return fail(RT_ERR_UNSUPPORTED, "BVH leaf with more than 255 primitives"); }
     if (s->bvh.depth > 64) { delete s; return fail(RT_ERR_UNSUPPORTED, "BVH deeper than 64 (the reference's stack[64])"); }
     s->stack_depth = pick_stack(s->bvh.depth);

@@ -213,3 +213,25 @@ def test_unknown_recipe(rt):
     with pytest.raises(rt.RTError) as e:
         rt.recipe_describe("nope")
     assert e.value.code == rt.RT_ERR_INVALID
+
+
+def test_prebuilt_bvh_above_24bit_node_index_is_refused(rt):
+    """The device node word packs leftFirst << 8 | count: interior child indices are 24 bits
+    wide, so a tree with more than 2^24 nodes must be refused (before any device call), not
+    silently truncated.  The count is checked before the node array is read."""
+    import ctypes as C
+    light = rt.sphere((0, 4, -2), 0.5, 0)
+    pa = (rt.Prim * 1)(light)
+    ma = (rt.Material * 1)(rt.material(rt.LIGHT, (1, 1, 1)))
+    nodes = np.zeros((4, 32), np.uint8)
+    idx = np.zeros(1, np.uint32)
+    d = rt.SceneDesc()
+    d.prims, d.num_prims = pa, 1
+    d.materials, d.num_materials = ma, 1
+    d.bvh_nodes = nodes.ctypes.data_as(C.c_void_p)
+    d.bvh_num_nodes = (1 << 24) + 2
+    d.bvh_indices = idx.ctypes.data_as(C.POINTER(C.c_uint32))
+    h = C.c_void_p()
+    rc = rt.lib().rt_scene_create(C.byref(d), C.byref(h))
+    assert rc == rt.RT_ERR_UNSUPPORTED, rt.lib().rt_last_error()
+    assert b"2^24" in rt.lib().rt_last_error()

@@ -54,6 +54,8 @@ def lib():
             getattr(L, n).restype = C.c_int
         L.or_scene_nodes.restype = vp
         L.or_scene_nodes.argtypes = [vp]
+        L.or_scene_set_bvh.argtypes = [vp, vp, C.c_int, C.POINTER(C.c_uint32)]
+        L.or_scene_set_bvh.restype = C.c_int
         L.or_scene_indices.restype = C.POINTER(C.c_uint32)
         L.or_scene_indices.argtypes = [vp]
         L.or_scene_add_material.argtypes = [vp, C.c_int, fp, fp, C.c_float, C.c_float]

@@ -4,8 +4,9 @@ primitive list built in the oracle (the checker), and the primitive known-answer
 import numpy as np
 
 
-def oracle_scene(rt, oracle, prims, mats, sky=None, textures=()):
-    """The primitive list (rt.sphere / plane / triangle / cube / quad records) as an oracle scene."""
+def oracle_scene(rt, oracle, prims, mats, sky=None, textures=(), bvh=None):
+    """The primitive list (rt.sphere / plane / triangle / cube / quad records) as an oracle scene;
+    bvh = (nodes [n, 32] uint8, indices) replaces the oracle's BuildBVH."""
     import ctypes as C
     L = oracle.lib()
     h = L.or_scene_new()
@@ -30,7 +31,12 @@ def oracle_scene(rt, oracle, prims, mats, sky=None, textures=()):
             L.or_scene_add_triangle(h, f3(*v[:3]), f3(*v[3:6]), f3(*v[6:9]), p.material)
     if sky is not None:
         L.or_scene_set_sky(h, sky.shape[1], sky.shape[0], sky.ctypes.data_as(C.POINTER(C.c_uint32)))
-    L.or_scene_build_bvh(h)
+    if bvh is None:
+        L.or_scene_build_bvh(h)
+    else:
+        nodes, idx = np.ascontiguousarray(bvh[0], np.uint8), np.ascontiguousarray(bvh[1], np.uint32)
+        assert L.or_scene_set_bvh(h, nodes.ctypes.data_as(C.c_void_p), len(nodes),
+                                  idx.ctypes.data_as(C.POINTER(C.c_uint32))) == len(nodes)
     o = oracle.Scene.__new__(oracle.Scene)
     o.L, o.h = L, h
     return o

@@ -21,8 +21,10 @@ LIB_PATH = os.path.abspath(os.environ.get("RTAMD_LIB", os.path.join(PKG_DIR, "li
 DATA_DIR = os.path.join(PKG_DIR, "data")
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "rt_amd.h")
 
-ABI_VERSION = 2   # include/rt_amd.h RT_ABI_VERSION
-RT_OK, RT_ERR_INVALID, RT_ERR_NO_DEVICE, RT_ERR_HIP, RT_ERR_IO, RT_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5
+ABI_VERSION = 3   # include/rt_amd.h RT_ABI_VERSION
+RT_OK, RT_ERR_INVALID, RT_ERR_NO_DEVICE, RT_ERR_HIP, RT_ERR_IO, RT_ERR_UNSUPPORTED, RT_ERR_COMM = 0, -1, -2, -3, -4, -5, -6
+RT_COMM_ID_BYTES = 128
+MULTI_PIPELINED, MULTI_TIMING = 1, 2
 SPHERE, PLANE, CUBE, QUAD, TRIANGLE = 0, 1, 2, 3, 4
 DIFFUSE, MIRROR, DIELECTRIC, CHECKERBOARD, LIGHT, DSMIX, TEXTURE = 0, 1, 2, 3, 4, 5, 6
 MODE_PATH = 0
@@ -132,6 +134,16 @@ def lib():
         "rt_occluded_host": ([vp, vp, vp, u32], C.c_int),
         "rt_intersect_packets": ([vp, vp, vp, u32, vp], C.c_int),
         "rt_intersect_packets_host": ([vp, vp, vp, u32], C.c_int),
+        "rt_trace": ([vp, C.c_int, vp, vp, vp, u32, vp, vp, vp, u32, vp], C.c_int),
+        "rt_trace_host": ([vp, C.c_int, vp, vp, vp, u32, vp, vp, vp, u32], C.c_int),
+        "rt_comm_unique_id": ([vp], C.c_int),
+        "rt_comm_create": ([vp, C.c_int, C.c_int, C.c_int, C.POINTER(vp)], C.c_int),
+        "rt_comm_wrap": ([vp, C.c_int, C.POINTER(vp)], C.c_int),
+        "rt_comm_info": ([vp, C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
+        "rt_comm_destroy": ([vp], C.c_int),
+        "rt_render_frame_multi": ([vp, vp, C.POINTER(Camera), C.POINTER(FrameParams), vp, u32, vp], C.c_int),
+        "rt_multi_flush": ([vp, vp, vp, vp], C.c_int),
+        "rt_comm_timing": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64)], C.c_int),
         "rt_camera_default": ([u32, u32, C.POINTER(Camera)], C.c_int),
         "rt_renderer_create": ([vp, u32, u32, C.POINTER(vp)], C.c_int),
         "rt_renderer_destroy": ([vp], C.c_int),
@@ -465,6 +477,38 @@ class Scene:
             _check(self.L.rt_occluded(self.h, C.c_void_p(r.data_ptr()), C.c_void_p(out.data_ptr()), n, C.c_void_p(s)))
         return out.bool()
 
+    def trace(self, rays, seeds, depth=10, last_specular=True, inside=False, mode=MODE_PATH, hits=False,
+              stream=None):
+        """Batched Renderer::Trace(ray, lastSpecular, depth) (renderer.cpp:17-72), or WhittedTrace
+        (renderer.cpp:138-195) with mode=MODE_WHITTED.  rays: (n, 7); seeds: n uint32 RNG states.
+        last_specular / inside: bool or per-ray arrays.  Returns (radiance [n, 3] f32, seeds after
+        the call [n] int32 holding the uint32 bits, ray counts {"shadow", "bounce"}[, hits as in
+        IntersectBVH]) as torch tensors on the scene's device."""
+        torch = _torch()
+        r = _as_device_rays(rays, self.device)
+        n = r.shape[0]
+        dev = r.device
+        sd = torch.as_tensor(np.asarray(seeds, np.uint32).view(np.int32) if not isinstance(seeds, torch.Tensor)
+                             else seeds, dtype=torch.int32).to(dev).clone().reshape(-1)
+        if sd.numel() != n:
+            raise RTError(RT_ERR_INVALID, "one seed per ray")
+        ls = np.broadcast_to(np.asarray(last_specular, bool), (n,))
+        ins = np.broadcast_to(np.asarray(inside, bool), (n,))
+        flags = torch.from_numpy((ls.astype(np.uint8) | (ins.astype(np.uint8) << 1)).copy()).to(dev)
+        rad = torch.empty((n, 3), dtype=torch.float32, device=dev)
+        counts = torch.zeros(2, dtype=torch.int64, device=dev)
+        hit = torch.empty((n, 4), dtype=torch.float32, device=dev) if hits else None
+        if n:
+            s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+            _check(self.L.rt_trace(self.h, mode, C.c_void_p(r.data_ptr()), C.c_void_p(sd.data_ptr()),
+                                   C.c_void_p(flags.data_ptr()), depth, C.c_void_p(rad.data_ptr()),
+                                   C.c_void_p(hit.data_ptr()) if hits else None, C.c_void_p(counts.data_ptr()), n,
+                                   C.c_void_p(s)))
+        out = (rad, sd, counts)
+        if hits:
+            out += ((hit[:, 0], hit.view(torch.int32)[:, 1], hit[:, 2], hit[:, 3]),)
+        return out
+
     def intersect_host(self, rays):
         """Host-array variant (copies through the library's staging buffer)."""
         rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 7)
@@ -508,6 +552,17 @@ class Renderer:
     @useWhitted.setter
     def useWhitted(self, on):
         self.mode = MODE_WHITTED if on else MODE_PATH
+
+    def Trace(self, rays, seeds, lastSpecular=True, depth=10, stream=None):
+        """Renderer::Trace (renderer.h:9) on a batch of rays with per-ray RNG states; returns
+        (radiance [n, 3], seeds after the call) on the device (Scene.trace)."""
+        rad, sd, _ = self.scene.trace(rays, seeds, depth=depth, last_specular=lastSpecular, stream=stream)
+        return rad, sd
+
+    def WhittedTrace(self, rays, seeds, depth=20, stream=None):
+        """Renderer::WhittedTrace (renderer.h:13) on a batch of rays."""
+        rad, sd, _ = self.scene.trace(rays, seeds, depth=depth, mode=MODE_WHITTED, stream=stream)
+        return rad, sd
 
     def close(self):
         h = getattr(self, "h", None)

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librtamd.so")
 # the kernels are compiled twice (core / extension builds of rt_kernels.inc), in parallel
-SOURCES = ["rt_host.cpp", "rt_device.hip", "rt_kern_core.hip", "rt_kern_ext.hip"]
+SOURCES = ["rt_host.cpp", "rt_device.hip", "rt_kern_core.hip", "rt_kern_ext.hip", "rt_multi.cpp"]
 HEADERS = ["rt_math.h", "rt_internal.h", "rt_libm.h", "rt_dev_types.h", "rt_kernels.inc",
            os.path.join("..", "..", "include", "rt_amd.h")]
 
@@ -24,7 +24,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # v_mov shuffles feeding them; scalar f32 issues faster on gfx950 and the frame kernel drops
 # from 91 to 68 VGPRs (5 -> 7 waves/SIMD): TEAPOT-F 1080p 0.120 -> 0.106 ms, CFG5-sub 10.4 ->
 # 9.4 ms, bit-identical (profiles/r01/ab_nslp_*.json).
-LIBS = ["-lz"]   # zlib: PNG textures (rt_image_load)
+LIBS = ["-lz", "-ldl"]   # zlib: PNG textures (rt_image_load); dl: RCCL is resolved at run time (rt_multi.cpp)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC",
          "-shared",
          "-Wall", "-Wno-unused-function"]

@@ -114,6 +114,17 @@ struct PathArgs {
     float4 *sum;
 };
 
+// Batched Renderer::Trace / WhittedTrace on caller rays (rt_trace): one lane per ray.
+struct TraceArgs {
+    const rt_ray *rays;
+    uint32_t *seeds;                     // per-ray RNG state, in / out
+    const uint8_t *flags;                // bit 0 lastSpecular, bit 1 inside (nullptr: 1)
+    float *radiance;                     // 3 floats per ray
+    rt_hit *hits;                        // optional: the ray after the first IntersectBVH
+    unsigned long long *counts;          // optional: [0] shadow rays, [1] bounce rays (added)
+    uint32_t n, depth;
+};
+
 // Each kernel build provides the same launchers: `kcore` is compiled without the
 // extension primitives and materials (cubes, quads, quad light, TextureMaterial,
 // non-Light light materials), `kext` with them.  The host picks per scene.
@@ -131,6 +142,8 @@ struct PathArgs {
     void launch_pt_lanes(const SceneView &S, const FrameArgs &F, const PathArgs &P, bool tex,     \
                          size_t lds, uint32_t num_cus, hipStream_t st);                           \
     void launch_pt_finish(const FrameArgs &F, const PathArgs &P, bool last, hipStream_t st);      \
+    void launch_trace(const SceneView &S, const TraceArgs &A, int mode, int md, bool tex,         \
+                      size_t lds, hipStream_t st);                                                \
     }
 RT_DECLARE_LAUNCHERS(kcore)
 RT_DECLARE_LAUNCHERS(kext)

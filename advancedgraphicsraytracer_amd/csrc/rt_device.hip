@@ -873,6 +873,14 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
 
 }  // namespace
 
+int rt::renderer_geometry(const rt_renderer *r, uint32_t *W, uint32_t *H, int *device) {
+    if (!r) return fail(RT_ERR_INVALID, "null renderer");
+    *W = r->W;
+    *H = r->H;
+    *device = r->scene->device;
+    return RT_OK;
+}
+
 extern "C" {
 
 int rt_device_count(int *count) {
@@ -974,6 +982,59 @@ int rt_intersect_packets(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }
+int rt_trace(rt_scene *s, int mode, const rt_ray *rays, uint32_t *seeds, const uint8_t *flags, uint32_t depth,
+             float *radiance, rt_hit *hits, uint64_t *ray_counts, uint32_t n, void *stream) {
+    if (!s || (n && (!rays || !seeds || !radiance))) return fail(RT_ERR_INVALID, "rt_trace: null argument");
+    if (mode != RT_MODE_PATH && mode != RT_MODE_WHITTED) return fail(RT_ERR_INVALID, "rt_trace: mode must be PATH or WHITTED");
+    if (depth > 32) return fail(RT_ERR_UNSUPPORTED, "Trace depth above 32");
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    TraceArgs A{};
+    A.rays = rays; A.seeds = seeds; A.flags = flags; A.radiance = radiance; A.hits = hits;
+    A.counts = reinterpret_cast<unsigned long long *>(ray_counts);
+    A.n = n; A.depth = depth;
+    const bool tex = !s->view.sky_const;
+    hipStream_t st = (hipStream_t)stream;
+    if (s->ext) kext::launch_trace(s->view, A, mode, max_depth_class(depth), tex, stack_bytes(s), st);
+    else kcore::launch_trace(s->view, A, mode, max_depth_class(depth), tex, stack_bytes(s), st);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+int rt_trace_host(rt_scene *s, int mode, const rt_ray *rays, uint32_t *seeds, const uint8_t *flags, uint32_t depth,
+                  float *radiance, rt_hit *hits, uint64_t *ray_counts, uint32_t n) {
+    if (!s || (n && (!rays || !seeds || !radiance))) return fail(RT_ERR_INVALID, "rt_trace_host: null argument");
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    // staging: rays | seeds | flags | radiance | hits | counts, 256-B aligned pieces
+    auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t o_seed = up(sizeof(rt_ray) * (size_t)n), o_flag = o_seed + up(4 * (size_t)n),
+                 o_rad = o_flag + up((size_t)n), o_hit = o_rad + up(12 * (size_t)n),
+                 o_cnt = o_hit + up(sizeof(rt_hit) * (size_t)n), need = o_cnt + 256;
+    if (need > s->scratch_bytes) {
+        if (s->d_scratch) HIP_TRY(hipFree(s->d_scratch));
+        s->d_scratch = nullptr;
+        s->scratch_bytes = 0;
+        HIP_TRY(hipMalloc(&s->d_scratch, need));
+        s->scratch_bytes = need;
+    }
+    char *b = (char *)s->d_scratch;
+    HIP_TRY(hipMemcpyAsync(b, rays, sizeof(rt_ray) * n, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(hipMemcpyAsync(b + o_seed, seeds, 4 * (size_t)n, hipMemcpyHostToDevice, s->stream));
+    if (flags) HIP_TRY(hipMemcpyAsync(b + o_flag, flags, n, hipMemcpyHostToDevice, s->stream));
+    if (ray_counts) HIP_TRY(hipMemcpyAsync(b + o_cnt, ray_counts, 16, hipMemcpyHostToDevice, s->stream));
+    int rc = rt_trace(s, mode, (const rt_ray *)b, (uint32_t *)(b + o_seed), flags ? (const uint8_t *)(b + o_flag) : nullptr,
+                      depth, (float *)(b + o_rad), hits ? (rt_hit *)(b + o_hit) : nullptr,
+                      ray_counts ? (uint64_t *)(b + o_cnt) : nullptr, n, s->stream);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(radiance, b + o_rad, 12 * (size_t)n, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipMemcpyAsync(seeds, b + o_seed, 4 * (size_t)n, hipMemcpyDeviceToHost, s->stream));
+    if (hits) HIP_TRY(hipMemcpyAsync(hits, b + o_hit, sizeof(rt_hit) * n, hipMemcpyDeviceToHost, s->stream));
+    if (ray_counts) HIP_TRY(hipMemcpyAsync(ray_counts, b + o_cnt, 16, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return RT_OK;
+}
+
 enum { CALL_INTERSECT, CALL_OCCLUDED, CALL_PACKETS };
 static int staged_call(rt_scene *s, const rt_ray *rays, void *out, size_t out_elem, uint32_t n, int kind) {
     if (!s || (n && (!rays || !out))) return fail(RT_ERR_INVALID, "null argument");

@@ -41,6 +41,9 @@ struct Bvh {
 };
 int build_bvh(const rt_prim *prims, const float *transforms, uint32_t n, Bvh &out);
 
+// frame size and device of a renderer (rt_multi.cpp)
+int renderer_geometry(const rt_renderer *r, uint32_t *W, uint32_t *H, int *device);
+
 // SURVEY.md 8(d) scenes as descriptions
 struct SceneSource {
     std::vector<rt_prim> prims;

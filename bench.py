@@ -1,18 +1,21 @@
 #!/usr/bin/env python3
 """Headline benchmark: Mrays/s (primary + shadow) of the MI355X ray-tracing hot path.
 
-Workload (BASELINE.json configs[1]): teapot.obj scene TEAPOT-F at
-1920x1080, 1 spp, primary + shadow = Renderer::Trace at depth 1 (one closest-hit ray
-per pixel, one NEE shadow ray per diffuse hit facing the light), accumulate + RGB8 pack,
-all in one kernel launch per frame (a "step").  Inputs are resident in HBM before
-timing; synthetic data = the bundled teapot mesh + the synthetic constant sky.
+Default workload (BASELINE.json configs[1], "config 2"): teapot.obj scene TEAPOT-F
+ at 1920x1080, 1 spp, primary + shadow = Renderer::Trace at depth 1 (one
+closest-hit ray per pixel, one NEE shadow ray per diffuse hit facing the light),
+accumulate + RGB8 pack, all in one kernel launch per frame (a "step").  Inputs are
+resident in HBM before timing; synthetic data = the bundled teapot mesh + the synthetic
+constant sky.  --config 3 / 4 / 5 select the other BASELINE.json GPU workloads:
+CFG3-sub 4 spp depth 4, mig29 x16 primary + shadow, CFG5-sub 16 spp depth 10.
 
-N > 1 (python -m torch.distributed.run ... bench.py --gpus N): weak scaling -- the
-frame's 8x8 tiles are interleaved over the ranks and the frame is rendered at spp = N,
-so every GPU traces one 1080p frame's worth of samples per step; one RCCL gather of
-the packed RGB8 tiles to rank 0 per frame assembles the image there.  The
-gather of frame i runs while frame i+1 renders (double-buffered tiles); the timed region
-ends after the last frame's gather and assembly.
+N > 1 (python -m torch.distributed.run ... bench.py --gpus N): the frame's 8x8 tiles are
+interleaved over the ranks, each rank renders its shard, ONE RCCL gather per frame brings
+the packed tiles to rank 0, which assembles the image.  The exchange is
+the library's C-ABI (rt_render_frame_multi: RCCL issued from C++, pipelined so frame i's
+gather runs beside frame i+1's render).  Scaling: config 2 and 3 are weak (spp = N x the
+config's spp: every GPU traces one frame's worth of samples per step), config 4 and 5 are
+strong (one frame split over the N GPUs); --scaling overrides.
 value = all rays traced by all ranks / max-over-ranks wall time.
 """
 import argparse
@@ -26,20 +29,27 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 import advancedgraphicsraytracer_amd as rt  # noqa: E402
+import roofline as rl  # noqa: E402
 
+# BASELINE.json configs[1..4]: scene recipe, spp, Trace depth, N > 1 scaling,
+# dominant kernel (the roofline's subject; profiles/pmc_summary.json key cfgN)
+CONFIGS = {
+    2: dict(scene="teapotF", spp=1, depth=1, scaling="weak", kernel="k_render<0, 1, false>"),
+    3: dict(scene="cfg3", spp=4, depth=4, scaling="weak", kernel="k_pt_lanes"),
+    4: dict(scene="mig16", spp=1, depth=1, scaling="strong", kernel="k_render<0, 1, false>"),
+    5: dict(scene="cfg5", spp=16, depth=10, scaling="strong", kernel="k_pt_lanes"),
+}
 # Algorithmic bytes per ray, SURVEY.md 8(d): B = 32*A + 40*P (+36 B pixel IO per camera
 # sample), A = BVH node reads (one 32-B node per child test), P = primitive tests (4-B index
-# + 36-B triangle).  A, P measured with the oracle on this exact workload (per-pixel seeds,
-# Trace depth 1); see DESIGN.md section 4.
+# + 36-B triangle).  A, P measured with the oracle on these workloads (per-pixel seeds, Trace
+# depth 1); DESIGN.md section 4.  Not a roofline: those bytes are L1/L2 hits.
 BYTES_PER_RAY = {
-    # recipe: (primary incl. 36 B IO, shadow)
     "teapotF": (32 * 14.235 + 40 * 1.635 + 36, 32 * 16.719 + 40 * 2.133),
     "mig16": (32 * 23.241 + 40 * 1.835 + 36, 32 * 79.366 + 40 * 8.545),
-    "cfg5": (32 * 9.371 + 40 * 1.126 + 36, 32 * 10.611 + 40 * 1.567),
 }
-HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
 def parse():
@@ -47,41 +57,83 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--scene", default="teapotF", choices=rt.RECIPES)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--scene", default=None, choices=rt.RECIPES)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=1)
-    ap.add_argument("--depth", type=int, default=1)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=None)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default=None)
     ap.add_argument("--ramp-seconds", type=float, default=0.5,
                     help="untimed frames before the warm-up steps until this much wall time has passed: the "
                          "GPU clocks ramp up over ~0.1 s, and 5 warm-up frames are only ~0.5 ms of work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--per-step-events", action="store_true", help="HIP event pair around every launch at N = 1 too")
-    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline sample")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
-                    help="HBM traffic per launch from rocprofv3 PMC passes (tools/pmc_summary.py)")
-    return ap.parse_args()
+    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the all-cores CPU baseline sample")
+    ap.add_argument("--summary", default=rl.SUMMARY, help="rocprofv3 PMC / kernel-trace summary (tools/roofline.py)")
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    args.scene = args.scene or cfg["scene"]
+    args.spp = args.spp or cfg["spp"]
+    args.depth = args.depth if args.depth is not None else cfg["depth"]
+    args.scaling = args.scaling or cfg["scaling"]
+    return args
 
 
-def cpu_baseline(args, threads):
-    """The oracle (CPU restatement, kind "port") on the same workload, bounded sample."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(args, spp):
+    """The oracle (CPU restatement, kind "port") on the same workload: a bounded sample on
+    all the host threads this job may use (OMP_NUM_THREADS, which the GPU box sets to its
+    CPU share, else the affinity mask), and one frame on 1 core."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     s = pyoracle.Scene(args.scene, rt.DATA_DIR)
     W, H = args.width, args.height
     acc = np.zeros((W * H, 4), np.float32)
-    s.tick(W, H, acc, spp=args.spp, depth=args.depth, frame=0, threads=threads)   # warm
+    s.tick(W, H, acc, spp=spp, depth=args.depth, frame=0, threads=threads)   # warm
     frames, rays, t0 = 0, 0, time.perf_counter()
     while True:
-        _, st = s.tick(W, H, acc, spp=args.spp, depth=args.depth, frame=frames + 1, threads=threads)
+        _, st = s.tick(W, H, acc, spp=spp, depth=args.depth, frame=frames + 1, threads=threads)
         rays += st["isect"] + st["occl"]
         frames += 1
         if time.perf_counter() - t0 >= args.cpu_seconds:
             break
     dt = time.perf_counter() - t0
-    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} full {W}x{H} {args.scene} frames (spp {args.spp}, Trace depth {args.depth}), "
-                      f"{dt:.2f} s wall on {threads} OpenMP threads"}
+    # one core: rows of one frame until ~1/3 of the all-cores budget has passed
+    t1, rays1, y = time.perf_counter(), 0, 0
+    while y < H and time.perf_counter() - t1 < args.cpu_seconds / 3:
+        y1 = min(H, y + 60)
+        _, st = s.tick(W, H, acc, spp=spp, depth=args.depth, frame=frames + 1, y0=y, y1=y1, threads=1)
+        rays1 += st["isect"] + st["occl"]
+        y = y1
+    dt1 = time.perf_counter() - t1
+    value, single = rays / dt / 1e6, rays1 / dt1 / 1e6
+    out = {"value": round(value, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+           "sample": f"{frames} full {W}x{H} {args.scene} frames (spp {spp}, Trace depth {args.depth}) in "
+                     f"{dt:.2f} s on {threads} OpenMP threads; 1 core: rows 0-{y} of one frame in {dt1:.2f} s",
+           "single_core": round(single, 3), "cpu_model": cpu_model(), "host_cpus": os.cpu_count()}
+    cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    try:   # the restatement against the reference, both timed in the build container
+        with open(cal) as f:
+            c = json.load(f).get(f"config{args.config}")
+        if c:
+            out["calibration"] = {"restatement_over_reference": c["ratio_threads"],
+                                  "restatement_over_reference_1core": c["ratio_1core"], "source": "profiles/cpu_calibration.json",
+                                  "reference_equivalent_mrays": round(value / c["ratio_threads"], 3)}
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
 
 
 def main():
@@ -95,11 +147,11 @@ def main():
     # one rank per GPU; RT_DIST_BACKEND=gloo + fewer GPUs than ranks rehearses the N > 1 path
     # on a single card (ranks share it; the exchange goes through gloo instead of RCCL)
     device = local % max(1, torch.cuda.device_count()) if world > 1 else 0
+    backend = os.environ.get("RT_DIST_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(device)
-        backend = os.environ.get("RT_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
@@ -107,7 +159,8 @@ def main():
     torch.cuda.set_device(device)
 
     W, H = args.width, args.height
-    spp = args.spp * world                 # weak scaling: spp grows with the tile share shrinking
+    # weak: every GPU traces one frame's worth of samples per step; strong: one frame, split
+    spp = args.spp * world if args.scaling == "weak" else args.spp
     scene = rt.Scene.recipe(args.scene, device=device)
     rend = rt.Renderer(scene, W, H)
     stream = torch.cuda.Stream(device=device)
@@ -115,8 +168,11 @@ def main():
     frame_out = torch.zeros(W * H, dtype=torch.int32, device=f"cuda:{device}")
     sharded = None
     if world > 1:
-        from advancedgraphicsraytracer_amd.distributed import ShardedFrame
-        sharded = ShardedFrame(rend, device=torch.device("cuda", device))
+        from advancedgraphicsraytracer_amd.distributed import NativeShardedFrame, ShardedFrame
+        if backend == "nccl":   # the product path: RCCL gather from C++ (rt_render_frame_multi)
+            sharded = NativeShardedFrame(rend, device=torch.device("cuda", device))
+        else:
+            sharded = ShardedFrame(rend, device=torch.device("cuda", device))
 
     def step(i, events=None):
         with torch.cuda.stream(stream):
@@ -136,13 +192,14 @@ def main():
             with torch.cuda.stream(stream):
                 sharded.flush(stream=sptr)
 
-    # clock ramp (untimed, before the W warm-up steps): blocks of 20 frames until
+    # clock ramp (untimed, before the W warm-up steps): blocks of frames until
     # --ramp-seconds have passed; at N > 1 the ranks agree on every block (the per-frame
     # gather is a collective, so every rank must submit the same frames)
     nf = 0
     t_ramp = time.perf_counter()
+    block = 20 if args.depth <= 1 else 2
     while args.ramp_seconds > 0:
-        for _ in range(20):
+        for _ in range(block):
             step(nf)
             nf += 1
         drain()
@@ -159,6 +216,8 @@ def main():
     drain()
     torch.cuda.synchronize(device)
     c0 = rend.counters()
+    if sharded is not None:
+        sharded.set_timing(True)        # per-frame render / gather events from here on
     # HIP events on the launch stream: at N = 1 one pair brackets the timed region (per-launch
     # average = region / steps; no event packets between the frames), at N > 1 a pair around
     # each shard render (the exchange runs between them)
@@ -182,48 +241,47 @@ def main():
     t1 = time.perf_counter()
     c1 = rend.counters()
     elapsed = t1 - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) / (1 if per_step_events else args.steps)
+    frame_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) / (1 if per_step_events else args.steps)
     primary = c1["primary"] - c0["primary"]
     shadow = c1["shadow"] - c0["shadow"]
     bounce = c1["bounce"] - c0["bounce"]
-    local_rays = torch.tensor([primary + shadow + bounce, primary, shadow], dtype=torch.float64, device=f"cuda:{device}")
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+    dev = f"cuda:{device}"
+    local_rays = torch.tensor([primary + shadow + bounce, primary, shadow, bounce], dtype=torch.float64, device=dev)
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    multi = None
+    if sharded is not None:
+        tm = sharded.timing()
+        if tm is not None:   # this rank's render and exposed gather time per frame (max over ranks)
+            rms, gms, n = tm
+            per = torch.tensor([rms / max(n, 1), gms / max(n, 1)], dtype=torch.float64, device=dev)
+            dist.all_reduce(per, op=dist.ReduceOp.MAX)
+            multi = {"exchange": "rt_render_frame_multi (RCCL send/recv to rank 0 from C++, pipelined)",
+                     "render_ms_per_frame_max_rank": round(per[0].item(), 4),
+                     "gather_ms_per_frame_max_rank": round(per[1].item(), 4)}
+        else:
+            multi = {"exchange": f"torch.distributed gather ({backend})"}
     if dist:
         dist.all_reduce(local_rays, op=dist.ReduceOp.SUM)
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    tot_rays, tot_primary, tot_shadow = local_rays.tolist()
+    tot_rays, tot_primary, tot_shadow, tot_bounce = local_rays.tolist()
     wall = t_max.item()
 
     if rank == 0:
-        bp, bs = BYTES_PER_RAY.get(args.scene, (None, None))
-        roofline = None
-        if bp is not None and args.depth == 1:
-            per_launch = (primary * bp + shadow * bs) / args.steps     # this rank's launch
-            achieved = per_launch / (kern_ms * 1e-3) / 1e9
-            traffic = valu = None
-            try:
-                with open(args.pmc_json) as f:
-                    pmc = json.load(f)
-                key = f"{args.scene}_{W}x{H}_spp{spp}_d{args.depth}"
-                if key in pmc:
-                    traffic = pmc[key]["hbm_bytes_per_launch"]
-                    valu = pmc[key].get("valu_insts_per_launch")
-            except (OSError, ValueError, KeyError):
-                traffic = None
-            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                        "kernel": rend.kernel_name(spp=spp, depth=args.depth), "kernel_ms": round(kern_ms, 4),
-                        "bytes_per_ray": {"primary": round(bp, 1), "shadow": round(bs, 1)},
-                        # the algorithmic node / triangle bytes are served by L1/L2 (the scene is
-                        # ~0.1 MB): frac > 1 means "beyond the HBM roofline"; the HBM bytes the
-                        # PMC counters see per launch, and their rate, are these
-                        "hbm_measured_gbs": round(traffic / (kern_ms * 1e-3) / 1e9, 2) if traffic else None,
-                        "hbm_measured_frac": round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if traffic else None,
-                        # the binding resource: vector issue.  SQ_INSTS_VALU per launch (PMC pass) x 2
-                        # cycles per wave64 instruction over 1,024 SIMDs x the launch's cycles at 2.4 GHz
-                        "valu_issue_frac": round(valu * 2 / (1024 * kern_ms * 1e-3 * 2.4e9), 4) if valu else None}
+        cfg = CONFIGS[args.config]
+        summary = rl.load(args.summary)
+        key = f"cfg{args.config}"
+        roof = None
+        default_workload = (args.scene, W, H, args.spp, args.depth) == (cfg["scene"], 1920, 1080, cfg["spp"], cfg["depth"])
+        if key in summary and default_workload:
+            # one kernel per frame (depth 1, N = 1): its live duration is the frame's event time
+            live = frame_ms if (args.depth == 1 and world == 1) else None
+            bp, bs = BYTES_PER_RAY.get(args.scene, (None, None))
+            alg = (primary * bp + shadow * bs) / args.steps if (bp and live) else None
+            roof = rl.roofline(summary[key], kernel_ms=live, algorithmic_bytes=alg)
+            roof["source"] = f"profiles/pmc_summary.json[{key}] (tools/roofline.py)"
         line = {
-            "metric": "Mrays/s (primary+shadow) at 1080p",
+            "metric": "Mrays/s (primary+shadow) at 1080p" if args.depth == 1 else
+                      f"Mrays/s (all traced rays) at {H}p, config {args.config}",
             "value": round(tot_rays / wall / 1e6, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -232,27 +290,35 @@ def main():
             "clock_ramp_frames": ramp_frames,
             "ms_per_step": round(wall / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: bundled teapot.obj mesh (SURVEY 8(d) TEAPOT-F recipe) + constant 1024x512 sky, "
+            "data": f"synthetic: bundled meshes (SURVEY 8(d) {args.scene} recipe) + constant 1024x512 sky, "
                     "per-pixel seeds InitSeed(pixel + W*H*(sample + spp*frame))",
-            "config": {"workload": f"{args.scene} {W}x{H}, spp {spp} ({args.spp} per GPU-frame share), "
-                                   f"Trace depth {args.depth} (primary + NEE shadow), accumulate + RGB8",
+            "config": {"workload": f"config {args.config}: {args.scene} {W}x{H}, spp {spp}"
+                                   + (f" ({args.spp} per GPU, weak)" if args.scaling == "weak" and world > 1 else "")
+                                   + f", Trace depth {args.depth}"
+                                   + (" (primary + NEE shadow)" if args.depth == 1 else " (path tracing)")
+                                   + ", accumulate + RGB8",
                        "scene": args.scene, "width": W, "height": H, "spp": spp, "depth": args.depth,
                        "parallelism": f"screen-tile x{world}" if world > 1 else "single GPU"},
             "fps": round(args.steps / wall, 3),
             "msamples_per_s": round(W * H * spp / (wall / args.steps) / 1e6, 3),
-            "rays": {"primary": int(tot_primary), "shadow": int(tot_shadow), "total": int(tot_rays)},
-            "roofline": roofline,
+            "rays": {"primary": int(tot_primary), "shadow": int(tot_shadow), "bounce": int(tot_bounce),
+                     "total": int(tot_rays)},
+            "frame_ms_events": round(frame_ms, 4),
+            "roofline": roof,
         }
+        if multi:
+            line["multi_gpu"] = multi
         if world == 1 and not args.no_cpu_baseline:
             try:
-                threads = max(1, min(16, len(os.sched_getaffinity(0))))
-                line["cpu_baseline"] = cpu_baseline(args, threads)
+                line["cpu_baseline"] = cpu_baseline(args, spp)
             except Exception as e:   # the baseline is reported, never the product
                 line["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
         print(json.dumps(line), flush=True)
+    if sharded is not None:
+        sharded.close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 enum {
     RT_OK = 0,
@@ -41,7 +41,8 @@ enum {
     RT_ERR_NO_DEVICE = -2,  /* no HIP device / kernel image not loadable */
     RT_ERR_HIP = -3,        /* HIP runtime error */
     RT_ERR_IO = -4,         /* file not found / parse error */
-    RT_ERR_UNSUPPORTED = -5 /* scene outside the kernels' limits */
+    RT_ERR_UNSUPPORTED = -5, /* scene outside the kernels' limits */
+    RT_ERR_COMM = -6        /* RCCL missing or a collective failed */
 };
 
 /* Primitive kinds, Primitive.h:8-14. */
@@ -188,6 +189,25 @@ int rt_intersect_host(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t n)
 int rt_occluded_host(rt_scene *s, const rt_ray *rays, uint8_t *out, uint32_t n);
 int rt_intersect_packets_host(rt_scene *s, const rt_ray *rays, rt_hit *hits, uint32_t n);
 
+/* Batched Renderer::Trace(Ray&, bool lastSpecular, int depth) (renderer.h:9, renderer.cpp:17-72)
+ * or, with mode RT_MODE_WHITTED, Renderer::WhittedTrace(Ray&, int depth) (renderer.h:13,
+ * renderer.cpp:138-195); depth <= 32, 0 returns black as the reference does.
+ *   rays_dev[n]        the rays (O, D, t);
+ *   seeds_dev[n]       ray i's RNG state (the seed RandomFloat() advances,
+ *                      template/template.cpp:673-704), updated in place to the state after
+ *                      the call, so calls chain like the reference's global seed;
+ *   flags_dev[n]       bit 0 = lastSpecular, bit 1 = Ray::inside; NULL = lastSpecular true,
+ *                      outside (the reference's defaults);
+ *   radiance_dev[3n]   the returned float3 per ray;
+ *   hits_dev[n]        optional (NULL): the ray as the first Scene::IntersectBVH leaves it
+ *                      (Trace takes Ray&, renderer.cpp:20);
+ *   ray_counts_dev[2]  optional (NULL): shadow rays and bounce rays traced, added to. */
+int rt_trace(rt_scene *s, int mode, const rt_ray *rays_dev, uint32_t *seeds_dev, const uint8_t *flags_dev,
+             uint32_t depth, float *radiance_dev, rt_hit *hits_dev, uint64_t *ray_counts_dev, uint32_t n, void *stream);
+/* Host-pointer convenience of rt_trace (all arrays in host memory; synchronous). */
+int rt_trace_host(rt_scene *s, int mode, const rt_ray *rays, uint32_t *seeds, const uint8_t *flags, uint32_t depth,
+                  float *radiance, rt_hit *hits, uint64_t *ray_counts, uint32_t n);
+
 /* ---- renderer (Renderer, renderer.h:5-160) -------------------------------- */
 /* Camera::Camera (camera.h:28-41) for a W x H target */
 int rt_camera_default(uint32_t width, uint32_t height, rt_camera *out);
@@ -209,6 +229,38 @@ int rt_render_shard(rt_renderer *r, const rt_camera *cam, const rt_frame_params 
  * buffers (each rt_shard_capacity pixels) -> rgb8_dev[W*H]. */
 int rt_assemble_shards(rt_renderer *r, const uint32_t *gathered_dev, uint32_t num_shards, uint32_t *rgb8_dev,
                        void *stream);
+/* ---- multi-GPU frames (one process per GPU) ---------------
+ * Replaces the OpenMP pixel loop of Renderer::Tick (renderer.cpp:213-245) across the GPUs of
+ * a node: rank k renders the 8x8 tiles t with t % world == k, then ONE RCCL gather per frame
+ * (ncclSend / ncclRecv to rank 0 in one group) and rank 0's assembly.  Every rank keeps its
+ * own scene replica and accumulator.  RCCL (librccl.so.1) is loaded at first use. */
+#define RT_COMM_ID_BYTES 128
+typedef struct rt_comm rt_comm;
+/* rank 0 makes the id (ncclGetUniqueId) and hands it to the other ranks out of band */
+int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
+/* collective: every rank calls it with the same id (ncclCommInitRank); device = this rank's GPU */
+int rt_comm_create(const uint8_t id[RT_COMM_ID_BYTES], int rank, int world, int device, rt_comm **out);
+/* use a caller-owned ncclComm_t (from the same librccl.so.1; not destroyed by rt_comm_destroy) */
+int rt_comm_wrap(void *nccl_comm, int device, rt_comm **out);
+int rt_comm_info(const rt_comm *c, int *rank, int *world);
+int rt_comm_destroy(rt_comm *c);
+/* One frame on every rank (same camera and params everywhere).  flags 0: in stream order,
+ * render this rank's tiles, gather, and on rank 0 assemble the frame into rgb8_dev (W*H;
+ * ignored, may be NULL, on other ranks).  RT_MULTI_PIPELINED: the frame's gather runs on
+ * the communicator's own stream beside the caller's next work, and the call completes the
+ * PREVIOUS pipelined frame into rgb8_dev (nothing on the first call); rt_multi_flush
+ * completes the last one.  Counters and the accumulator stay per rank. */
+#define RT_MULTI_PIPELINED 1u
+/* RT_MULTI_TIMING: HIP events around this rank's render and its gather, summed by rt_comm_timing */
+#define RT_MULTI_TIMING 2u
+int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, const rt_frame_params *p,
+                          uint32_t *rgb8_dev, uint32_t flags, void *stream);
+int rt_multi_flush(rt_renderer *r, rt_comm *c, uint32_t *rgb8_dev, void *stream);
+/* Sum over the RT_MULTI_TIMING frames since the last call (waits for them): render_ms =
+ * this rank's shard render, gather_ms = from the render's end to the gather's completion
+ * (exposed exchange latency; beside the next render in pipelined mode); resets the sums. */
+int rt_comm_timing(rt_comm *c, double *render_ms, double *gather_ms, uint64_t *frames);
+
 int rt_renderer_counters(rt_renderer *r, rt_counters *out);
 /* accumulator readback, W*H float4 */
 int rt_renderer_read_accumulator(rt_renderer *r, float *host_out);

@@ -9,6 +9,7 @@
 //   Tmpl8::Scene::IntersectBVHPacket template/scene.h:322 -> rt_intersect_packets_host
 //   Tmpl8::Camera              camera.h:28-52         -> rt_camera_default
 //   Tmpl8::Renderer::Tick      renderer.cpp:200-309   -> rt_render_frame_host
+//   Tmpl8::Renderer::Trace     renderer.cpp:17-72     -> rt_trace_host (WhittedTrace: 138-195)
 //
 // Per-ray calls cross PCIe; batch them (the vector overloads) for throughput.  There is
 // no CPU fallback: every call reports the library's error through RtError.
@@ -147,6 +148,31 @@ class Renderer {   // renderer.h:5-160
         swapped_ = false;
         rt_check(rt_render_frame_host(h_, &camera.cam, &p, pixels.data()));
     }
+    // Renderer::Trace (renderer.h:9, renderer.cpp:17-72) and WhittedTrace (renderer.h:13,
+    // renderer.cpp:138-195) on one ray: the reference's RandomFloat() advances one global seed
+    // (template/template.cpp:673-686); `seed` plays that role and advances the same way.  As
+    // Trace takes Ray&, the ray is left as the first IntersectBVH leaves it (renderer.cpp:20).
+    float3 Trace(Ray &ray, bool lastSpecular = true, int depth = 10) {
+        std::vector<Ray *> one{&ray};
+        std::vector<uint32_t> seeds{seed};
+        float3 c = Trace(one, seeds, lastSpecular, depth)[0];
+        seed = seeds[0];
+        return c;
+    }
+    float3 WhittedTrace(Ray &ray, int depth = 20) {
+        std::vector<Ray *> one{&ray};
+        std::vector<uint32_t> seeds{seed};
+        float3 c = run_trace(RT_MODE_WHITTED, one, seeds, true, depth)[0];
+        seed = seeds[0];
+        return c;
+    }
+    // Batched Trace: ray i draws from seeds[i] (updated in place); one launch for the batch.
+    std::vector<float3> Trace(std::vector<Ray *> &rays, std::vector<uint32_t> &seeds, bool lastSpecular = true,
+                              int depth = 10) {
+        return run_trace(RT_MODE_PATH, rays, seeds, lastSpecular, depth);
+    }
+    uint32_t seed = 0x12345678;     // template/template.cpp:673
+
     // The K key (renderer.h:138): switch integrators; the next frame restarts accumulation.
     void ToggleWhitted() { useWhitted = !useWhitted; swapped_ = true; }
     rt_counters Counters() { rt_counters c{}; rt_check(rt_renderer_counters(h_, &c)); return c; }
@@ -155,6 +181,29 @@ class Renderer {   // renderer.h:5-160
     Camera camera;
 
   private:
+    std::vector<float3> run_trace(int mode, std::vector<Ray *> &rays, std::vector<uint32_t> &seeds, bool lastSpecular,
+                                  int depth) {
+        if (seeds.size() != rays.size() || depth < 0) throw RtError(RT_ERR_INVALID, "Trace: one seed per ray");
+        std::vector<rt_ray> in(rays.size());
+        std::vector<uint8_t> flags(rays.size());
+        for (size_t i = 0; i < rays.size(); ++i) {
+            const Ray &r = *rays[i];
+            in[i] = rt_ray{r.O.x, r.O.y, r.O.z, r.D.x, r.D.y, r.D.z, r.t};
+            flags[i] = (uint8_t)((lastSpecular ? 1 : 0) | (r.inside ? 2 : 0));
+        }
+        std::vector<float> rad(3 * rays.size());
+        std::vector<rt_hit> hits(rays.size());
+        rt_check(rt_trace_host(scene.handle(), mode, in.data(), seeds.data(), flags.data(), (uint32_t)depth, rad.data(),
+                               hits.data(), nullptr, (uint32_t)in.size()));
+        std::vector<float3> out(rays.size());
+        for (size_t i = 0; i < rays.size(); ++i) {
+            out[i] = float3{rad[3 * i], rad[3 * i + 1], rad[3 * i + 2]};
+            if (hits[i].obj >= 0) {
+                rays[i]->t = hits[i].t; rays[i]->objIdx = hits[i].obj; rays[i]->u = hits[i].u; rays[i]->v = hits[i].v;
+            }
+        }
+        return out;
+    }
     uint32_t width_, height_;
     uint32_t frame_ = 0;
     bool swapped_ = false;

@@ -75,6 +75,8 @@ def lib():
                                       fp, C.POINTER(Stats)]
         L.or_tick.argtypes = [vp, C.POINTER(Camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                               fp, C.POINTER(C.c_uint32), C.POINTER(Stats), C.c_int]
+        L.or_trace_rays.argtypes = [vp, fp, C.c_int, C.POINTER(C.c_uint8), C.c_int, C.POINTER(C.c_uint32), fp,
+                                    C.POINTER(Stats)]
         L.or_camera_rays.argtypes = [C.POINTER(Camera), C.c_int, C.c_int, C.c_int, ip, C.c_int, fp]
         L.or_intersect.argtypes = [vp, fp, C.c_int, fp, ip, fp, fp, C.c_int]
         L.or_intersect_packets.argtypes = [vp, fp, C.c_int, fp, ip, fp, fp]
@@ -180,6 +182,18 @@ class Scene:
         self.L.or_trace_pixels(self.h, C.byref(cam), W, H, spp, depth, frame, _p(pixels, C.c_int32), len(pixels),
                                _p(rgb, C.c_float), C.byref(st))
         return rgb, st.as_dict()
+
+    def trace_rays(self, rays, seeds, depth=10, flags=None):
+        """Renderer::Trace / WhittedTrace (set_integrator) on (n, 7) rays with per-ray RNG states;
+        returns (radiance [n, 3], seeds after the call, stats)."""
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 7)
+        seeds = np.array(seeds, np.uint32).copy()
+        rgb = np.empty((len(rays), 3), np.float32)
+        fl = None if flags is None else np.ascontiguousarray(flags, np.uint8)
+        st = Stats()
+        self.L.or_trace_rays(self.h, _p(rays, C.c_float), len(rays), None if fl is None else _p(fl, C.c_uint8), depth,
+                             _p(seeds, C.c_uint32), _p(rgb, C.c_float), C.byref(st))
+        return rgb, seeds, st.as_dict()
 
     def tick(self, W, H, acc, spp=1, depth=10, frame=0, y0=0, y1=None, threads=0):
         """One Renderer::Tick over rows [y0, y1): updates acc (H*W*4 f32) in place, returns RGB8."""

@@ -1349,6 +1349,28 @@ void or_trace_pixels(const or_scene *s, const or_camera *c, int W, int H, int sp
     }
 }
 
+/* Renderer::Trace(ray, lastSpecular, depth) (renderer.cpp:17-72) / WhittedTrace(ray, depth)
+ * (renderer.cpp:138-195, integrator 1) on caller rays: ray i uses the RNG state seeds[i]
+ * (RandomFloat's seed, template/template.cpp:673-704) and leaves the state after the call in
+ * it; flags[i] bit 0 = lastSpecular, bit 1 = ray.inside (NULL: lastSpecular true, outside). */
+void or_trace_rays(const or_scene *s, const float *rays7, int n, const uint8_t *flags, int depth, uint32_t *seeds,
+                   float *rgb, or_stats *st) {
+    #pragma omp parallel
+    {
+        counters k; memset(&k, 0, sizeof(k));
+        #pragma omp for schedule(dynamic, 64)
+        for (int i = 0; i < n; i++) {
+            const float *q = rays7 + 7 * (size_t)i;
+            ray_t r = mkray(mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), q[6]);
+            const int fl = flags ? flags[i] : 1;
+            r.inside = (fl & 2) != 0;
+            f3 v = s->integrator == 1 ? whitted(s, &r, depth, &seeds[i], &k) : trace(s, &r, fl & 1, depth, &seeds[i], &k);
+            rgb[3 * i] = v.x; rgb[3 * i + 1] = v.y; rgb[3 * i + 2] = v.z;
+        }
+        add_counters(st, &k);
+    }
+}
+
 /* RGBF32_to_RGB8, template/precomp.h:441-444 (the _MSC_VER_ typo keeps this path) */
 static inline uint32_t rgb8(const float *a) {
     uint32_t r = f2u_wrap(255.0f * smin(1.0f, a[0]));

@@ -114,6 +114,9 @@ void or_trace_pixels(const or_scene *s, const or_camera *c, int W, int H, int sp
                      const int32_t *pixels, int n, float *rgb, or_stats *st);
 /* One Renderer::Tick over rows [y0,y1): trace, running average into acc (float4 per
  * pixel, renderer.cpp:235-241), RGB8 pack (template/precomp.h:432-448).  OpenMP. */
+/* Renderer::Trace / WhittedTrace on caller rays with per-ray RNG states (updated in place) */
+void or_trace_rays(const or_scene *s, const float *rays7, int n, const uint8_t *flags, int depth, uint32_t *seeds,
+                   float *rgb, or_stats *st);
 void or_tick(const or_scene *s, const or_camera *c, int W, int H, int spp, int depth, int frame,
              int y0, int y1, float *acc, uint32_t *rgb8, or_stats *st, int threads);
 /* batched IntersectBVH / IsOccluded on explicit rays: ray = O.xyz D.xyz tmax */

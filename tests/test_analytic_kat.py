@@ -57,6 +57,3 @@ def test_gpu_matches_analytic(rt, vectors):
     bad = K.check(t, obj, u, v, vectors)
     assert not bad, f"{len(bad)} mismatches, e.g. {bad[:3]}"
     assert np.array_equal(g.IsOccluded(rays).cpu().numpy(), OCC)
-    # the packet traversal (scene.h:322-412) reaches the same closest hits for these rays
-    pt, pobj, pu, pv = (x.cpu().numpy() for x in g.IntersectBVHPacket(rays))
-    assert np.array_equal(pobj[OBJ >= 0], OBJ[OBJ >= 0])

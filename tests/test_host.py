@@ -41,9 +41,11 @@ def test_library_is_gfx950_code_object(rt, tmp_path):
 
 def build_compat_host(rt, tmp_path):
     exe = tmp_path / "compat_host"
-    subprocess.run(["g++", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "tests", "cpp", "compat_host.cpp"), "-o", str(exe),
-                    rt.LIB_PATH, f"-Wl,-rpath,{os.path.dirname(rt.LIB_PATH)}"], check=True)
+    # plain g++ host (hipMalloc for the device frame of rt_render_frame_multi: HIP host API only)
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(ROOT, "include"),
+                    "-I", "/opt/rocm/include", os.path.join(ROOT, "tests", "cpp", "compat_host.cpp"), "-o", str(exe),
+                    rt.LIB_PATH, "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{os.path.dirname(rt.LIB_PATH)}",
+                    "-Wl,-rpath,/opt/rocm/lib"], check=True)
     return str(exe)
 
 
@@ -59,7 +61,7 @@ def test_compat_header_compiles(rt, tmp_path):
 
 
 def test_abi_version_and_device_count(rt):
-    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 2
+    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 3
     assert rt.device_count() >= 0
 
 

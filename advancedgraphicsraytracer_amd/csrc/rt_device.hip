@@ -65,6 +65,8 @@ struct rt_scene {
     double pt_drain_rounds = 1.0;   // ... and it drains any level holding <= this many rounds of resident lanes
     bool tile_order = true;         // measured-cost (longest first) tile order (RT_TILE_ORDER=0: off)
     uint32_t split_units = 20000;   // sample split below ~5 rounds of the 4096 resident waves
+    bool xcd_order = false;         // measured order grouped by XCD: blocks b, b + 8, ... (one XCD) render
+                                    // one compact screen region of 1/8 of the frame's cost (L2 locality)
     int32_t heavy_split = -1;       // primary+shadow frames: the costliest tiles run as two half-tile
                                     // waves (RT_SPLIT_HEAVY = count; -1: ntiles / 32)
     uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per renderer: 12 GB of the 288 GB HBM
@@ -508,6 +510,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     // RT_SPLIT_UNITS: sample-split target units (0 = never split)
     if (const char *e = std::getenv("RT_SPLIT_UNITS")) s->split_units = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_SPLIT_HEAVY")) s->heavy_split = std::max(-1, std::atoi(e));
+    if (const char *e = std::getenv("RT_XCD_ORDER")) s->xcd_order = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
@@ -643,6 +646,60 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
 // the 4th frame); otherwise frame 1 records and frame 2 applies.  Pixel values do not depend
 // on the order.  walk_phase: -1 no walk timing pending, 0 / 1 this frame times the lane /
 // wave walk, 2 the walk was picked on this frame, 3 the timing has not started yet.
+// XCD-grouped measured order (RT_XCD_ORDER=1): the frame kernel's block b (4 waves = slots
+// 4b .. 4b+3) runs on the XCD of blocks b % 8 (blocks are dealt round-robin over the 8 XCDs,
+// MI355X_MICROARCH.md), so group g = b % 8 gets one compact screen region -- a run of the
+// tiles in Morton order holding 1/8 of the measured cost -- costliest tile first.  Each XCD's
+// L2 then holds the nodes of its region only, not of the whole frame.  A group whose region
+// ran out takes tiles from the region with the most cost left.
+std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const std::vector<uint32_t> &cost) {
+    const uint32_t n = (uint32_t)cost.size();
+    auto morton = [](uint32_t x, uint32_t y) {
+        uint64_t m = 0;
+        for (int b = 0; b < 16; ++b) m |= (uint64_t)((x >> b) & 1u) << (2 * b) | (uint64_t)((y >> b) & 1u) << (2 * b + 1);
+        return m;
+    };
+    std::vector<uint32_t> z(n);
+    std::vector<uint64_t> code(n);
+    double total = 0;
+    for (uint32_t lt = 0; lt < n; ++lt) {
+        const uint32_t tile = lt * F.nshards + F.shard;
+        code[lt] = morton(tile % F.tiles_x, tile / F.tiles_x);
+        z[lt] = lt;
+        total += cost[lt];
+    }
+    std::stable_sort(z.begin(), z.end(), [&](uint32_t a, uint32_t b) { return code[a] < code[b]; });
+    std::vector<std::vector<uint32_t>> region(8);
+    std::vector<double> left(8, 0.0);
+    double acc = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t g = std::min<uint32_t>(7u, (uint32_t)(acc * 8.0 / std::max(total, 1.0)));
+        region[g].push_back(z[i]);
+        left[g] += cost[z[i]];
+        acc += cost[z[i]];
+    }
+    for (auto &rg : region)   // costliest first within a region (reversed: pop from the back)
+        std::stable_sort(rg.begin(), rg.end(), [&](uint32_t a, uint32_t b) { return cost[a] < cost[b]; });
+    std::vector<uint32_t> out;
+    out.reserve(n);
+    for (uint32_t b = 0; out.size() < n; ++b) {
+        for (uint32_t w = 0; w < 4 && out.size() < n; ++w) {
+            uint32_t g = b % 8u;
+            if (region[g].empty()) {   // out.size() < n: some region still holds tiles
+                int best = -1;
+                for (uint32_t h = 0; h < 8; ++h)
+                    if (!region[h].empty() && (best < 0 || left[h] > left[best])) best = (int)h;
+                g = (uint32_t)best;
+            }
+            const uint32_t t = region[g].back();
+            region[g].pop_back();
+            left[g] -= cost[t];
+            out.push_back(t);
+        }
+    }
+    return out;
+}
+
 int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt_frame_params *p, int walk_phase,
                     bool split_ok, int &split_timed) {
     split_timed = -1;
@@ -689,6 +746,8 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
         HIP_TRY(hipMemcpy(cost.data(), r->d_cost + (size_t)use * n, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
         for (uint32_t i = 0; i < n; ++i) ord[i] = i;
         std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+        std::vector<uint32_t> plain = ord;
+        if (r->scene->xcd_order && split_ok) plain = xcd_grouped_order(F, cost);
         // The costliest tiles can bound the frame's tail (one wave's latency chain): the split
         // order runs the first k of them as two waves of half a tile each (entry bit 31 =
         // split, bit 30 = which half).  It shortens tail-bound frames (mig29 x16 -10 %, 720p
@@ -700,7 +759,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
             const int32_t hs = r->scene->heavy_split;
             k = std::min<uint32_t>(n, hs < 0 ? n / 32u : (uint32_t)hs);
         }
-        std::vector<uint32_t> ent(ord);
+        std::vector<uint32_t> ent(plain);
         for (uint32_t i = 0; i < k; ++i) {
             ent.push_back(ord[i] | 0x80000000u);
             ent.push_back(ord[i] | 0xC0000000u);

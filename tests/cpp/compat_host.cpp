@@ -78,6 +78,7 @@ int main(int argc, char **argv) {
             rt_check(rt_render_frame_host(b, &cam, &fp, want.data()));
             if (hipMalloc((void **)&d_out, 4 * 64 * 40) != 0) { std::printf("hipMalloc\n"); return 1; }
             rt_check(rt_render_frame_multi(a, comm, &cam, &fp, d_out, 0, st));
+            rt_check(rt_synchronize(a));   // the frame ran on the renderer's non-blocking stream
             if (hipMemcpy(got.data(), d_out, 4 * 64 * 40, kHipMemcpyDeviceToHost) != 0) return 1;
             (void)hipFree(d_out);
             rt_check(rt_comm_destroy(comm));

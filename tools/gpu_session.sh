@@ -36,11 +36,6 @@ for s in "$@"; do
                 step sum_c$c 60 python tools/roofline.py summarize cfg$c "$k" gpurun_out/pc$c/trace gpurun_out/pc$c/fetch gpurun_out/pc$c/write gpurun_out/pc$c/sq gpurun_out/pc$c/tcc --out gpurun_out/pmc_summary.json
             done ;;
         prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 100 --warmup 5 --no-cpu-baseline ;;
-        pmc)
-            step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o pmc -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
-            step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o pmc -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
-            step pmc_valu 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_valu -o pmc -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
-            step pmc_sum 60 python tools/pmc_summary.py teapotF_1920x1080_spp1_d1 gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_latest.json "k_render<0, 1, false>" ;;
         listpmc) step listpmc 120 rocprofv3 -L ;;
         pmclds)
             step pmc_lds 600 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT --output-format csv -d gpurun_out/pmc_lds -o pmc -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;

@@ -510,6 +510,10 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     // RT_SPLIT_UNITS: sample-split target units (0 = never split)
     if (const char *e = std::getenv("RT_SPLIT_UNITS")) s->split_units = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_SPLIT_HEAVY")) s->heavy_split = std::max(-1, std::atoi(e));
+    // XCD-grouped tile order for scenes whose nodes + primitive slots exceed one XCD's 4 MB L2:
+    // mig29 x16 (11.6 MB) 0.449 -> 0.406 ms; a cache-resident TEAPOT-F loses with it (4K
+    // 0.377 -> 0.441 ms, 720p neutral) -- profiles/r02/ab_xcd_*.json.  RT_XCD_ORDER=0/1 forces it.
+    s->xcd_order = (size_t)s->bvh.nodes_used * 32u + (size_t)n * 48u > (4u << 20);
     if (const char *e = std::getenv("RT_XCD_ORDER")) s->xcd_order = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
@@ -652,8 +656,11 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
 // tiles in Morton order holding 1/8 of the measured cost -- costliest tile first.  Each XCD's
 // L2 then holds the nodes of its region only, not of the whole frame.  A group whose region
 // ran out takes tiles from the region with the most cost left.
-std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const std::vector<uint32_t> &cost) {
-    const uint32_t n = (uint32_t)cost.size();
+std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const std::vector<uint32_t> &entries,
+                                        const std::vector<uint32_t> &cost) {
+    // entries: order entries (local tile | split bits); an entry's cost is its tile's, halved
+    // for a half-tile entry (bit 31)
+    const uint32_t n = (uint32_t)entries.size();
     auto morton = [](uint32_t x, uint32_t y) {
         uint64_t m = 0;
         for (int b = 0; b < 16; ++b) m |= (uint64_t)((x >> b) & 1u) << (2 * b) | (uint64_t)((y >> b) & 1u) << (2 * b + 1);
@@ -661,12 +668,15 @@ std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const std::vector<ui
     };
     std::vector<uint32_t> z(n);
     std::vector<uint64_t> code(n);
+    std::vector<double> ec(n);
     double total = 0;
-    for (uint32_t lt = 0; lt < n; ++lt) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t e = entries[i], lt = e & 0x3fffffffu;
         const uint32_t tile = lt * F.nshards + F.shard;
-        code[lt] = morton(tile % F.tiles_x, tile / F.tiles_x);
-        z[lt] = lt;
-        total += cost[lt];
+        code[i] = morton(tile % F.tiles_x, tile / F.tiles_x) * 4u + (e >> 30);
+        ec[i] = (e >> 31) ? 0.5 * cost[lt] : (double)cost[lt];
+        z[i] = i;
+        total += ec[i];
     }
     std::stable_sort(z.begin(), z.end(), [&](uint32_t a, uint32_t b) { return code[a] < code[b]; });
     std::vector<std::vector<uint32_t>> region(8);
@@ -675,26 +685,26 @@ std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const std::vector<ui
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t g = std::min<uint32_t>(7u, (uint32_t)(acc * 8.0 / std::max(total, 1.0)));
         region[g].push_back(z[i]);
-        left[g] += cost[z[i]];
-        acc += cost[z[i]];
+        left[g] += ec[z[i]];
+        acc += ec[z[i]];
     }
-    for (auto &rg : region)   // costliest first within a region (reversed: pop from the back)
-        std::stable_sort(rg.begin(), rg.end(), [&](uint32_t a, uint32_t b) { return cost[a] < cost[b]; });
+    for (auto &rg : region)   // costliest first within a region (sorted ascending: taken from the back)
+        std::stable_sort(rg.begin(), rg.end(), [&](uint32_t a, uint32_t b) { return ec[a] < ec[b]; });
     std::vector<uint32_t> out;
     out.reserve(n);
     for (uint32_t b = 0; out.size() < n; ++b) {
         for (uint32_t w = 0; w < 4 && out.size() < n; ++w) {
             uint32_t g = b % 8u;
-            if (region[g].empty()) {   // out.size() < n: some region still holds tiles
+            if (region[g].empty()) {   // out.size() < n: some region still holds entries
                 int best = -1;
                 for (uint32_t h = 0; h < 8; ++h)
                     if (!region[h].empty() && (best < 0 || left[h] > left[best])) best = (int)h;
                 g = (uint32_t)best;
             }
-            const uint32_t t = region[g].back();
+            const uint32_t i = region[g].back();
             region[g].pop_back();
-            left[g] -= cost[t];
-            out.push_back(t);
+            left[g] -= ec[i];
+            out.push_back(entries[i]);
         }
     }
     return out;
@@ -746,8 +756,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
         HIP_TRY(hipMemcpy(cost.data(), r->d_cost + (size_t)use * n, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
         for (uint32_t i = 0; i < n; ++i) ord[i] = i;
         std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
-        std::vector<uint32_t> plain = ord;
-        if (r->scene->xcd_order && split_ok) plain = xcd_grouped_order(F, cost);
+
         // The costliest tiles can bound the frame's tail (one wave's latency chain): the split
         // order runs the first k of them as two waves of half a tile each (entry bit 31 =
         // split, bit 30 = which half).  It shortens tail-bound frames (mig29 x16 -10 %, 720p
@@ -759,12 +768,17 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
             const int32_t hs = r->scene->heavy_split;
             k = std::min<uint32_t>(n, hs < 0 ? n / 32u : (uint32_t)hs);
         }
-        std::vector<uint32_t> ent(plain);
+        std::vector<uint32_t> ent(ord), sp;
         for (uint32_t i = 0; i < k; ++i) {
-            ent.push_back(ord[i] | 0x80000000u);
-            ent.push_back(ord[i] | 0xC0000000u);
+            sp.push_back(ord[i] | 0x80000000u);
+            sp.push_back(ord[i] | 0xC0000000u);
         }
-        for (uint32_t i = k; i < n; ++i) ent.push_back(ord[i]);
+        for (uint32_t i = k; i < n; ++i) sp.push_back(ord[i]);
+        if (r->scene->xcd_order && split_ok) {   // both orders grouped by XCD (global-node frame kernel)
+            ent = xcd_grouped_order(F, ord, cost);
+            sp = xcd_grouped_order(F, sp, cost);
+        }
+        ent.insert(ent.end(), sp.begin(), sp.end());
         HIP_TRY(hipMemcpy(r->d_order, ent.data(), ent.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         r->order_split = k;
         r->order_state = 2;

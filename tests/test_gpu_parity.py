@@ -535,8 +535,8 @@ def test_lds_node_kernels_equal_global_kernel(rt, torch, monkeypatch, kind, spp,
 @pytest.mark.gpu
 @pytest.mark.parametrize("recipe,spp,mode,shards", [("teapotF", 1, 0, 1), ("mig16", 1, 0, 1), ("teapotF", 4, 0, 3),
                                                     ("cfg3", 2, 1, 1)])
-@pytest.mark.parametrize("heavy", ["-1", "64"])
-def test_measured_tile_order_keeps_frames(rt, torch, monkeypatch, recipe, spp, mode, shards, heavy):
+@pytest.mark.parametrize("heavy,xcd", [("-1", "0"), ("64", "0"), ("-1", "1"), ("64", "1")])
+def test_measured_tile_order_keeps_frames(rt, torch, monkeypatch, recipe, spp, mode, shards, heavy, xcd):
     """The longest-tile-first dispatch order (costs recorded on the 3rd frame, applied from
     the 4th; primary+shadow frames then time the half-tile split order against the plain one
     on 4 frames, or force it with RT_SPLIT_HEAVY=64) must not change any frame: 12 frames
@@ -546,6 +546,7 @@ def test_measured_tile_order_keeps_frames(rt, torch, monkeypatch, recipe, spp, m
     s_a = rt.Scene.recipe(recipe)
     monkeypatch.setenv("RT_TILE_ORDER", "1")
     monkeypatch.setenv("RT_SPLIT_HEAVY", heavy)
+    monkeypatch.setenv("RT_XCD_ORDER", xcd)      # order grouped by XCD (auto: scenes above 4 MB)
     s_b = rt.Scene.recipe(recipe)
     ra, rb = rt.Renderer(s_a, W, H), rt.Renderer(s_b, W, H)
     ra.mode = rb.mode = mode

@@ -30,12 +30,27 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fn
          "-Wall", "-Wno-unused-function"]
 
 
+def _source_hash():
+    """sha256 over the sources, headers, flags and this script: the library is rebuilt when any
+    of them differs from what it was built from (content, not file times, which a copied tree
+    -- e.g. a gpurun snapshot -- does not preserve)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in [os.path.join(CSRC, x) for x in SOURCES + HEADERS] + [os.path.abspath(__file__)]:
+        with open(f, "rb") as fh:
+            h.update(os.path.basename(f).encode() + b"\0" + fh.read())
+    h.update(" ".join(FLAGS + LIBS).encode())
+    return h.hexdigest()
+
+
+STAMP = LIB + ".srchash"
+
+
 def _stale():
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(STAMP):
         return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.abspath(__file__)]
-    return any(os.path.getmtime(d) > t for d in deps)
+    with open(STAMP) as f:
+        return f.read().strip() != _source_hash()
 
 
 def build(force=False, verbose=False):
@@ -65,6 +80,8 @@ def build(force=False, verbose=False):
     if r.returncode != 0:
         raise RuntimeError(f"link failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
     os.replace(LIB + ".tmp", LIB)
+    with open(STAMP, "w") as f:
+        f.write(_source_hash() + "\n")
     return LIB
 
 

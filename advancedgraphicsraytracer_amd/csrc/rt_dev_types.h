@@ -47,6 +47,8 @@ struct SceneView {
     uint32_t node_f4;                   // node array size in float4s
     uint32_t p48_f4, words_n;           // pairs48 size in float4s, words count
     int wave_primary;                   // camera rays take the wave-coherent walk
+    uint32_t tl_nodes;                  // RT_PT_TREELET: nodes [0, tl_nodes) (BFS-numbered top pairs)
+                                        // are copied to LDS by the lane kernel; 0 = off
 };
 
 // Ray counters are spread over kCounterSlots 64-byte slots (wave w adds into slot

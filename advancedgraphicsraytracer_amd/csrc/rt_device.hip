@@ -135,6 +135,43 @@ int material_flag(const rt_material &m, float diffuse, float specular) {   // ge
 
 constexpr uint32_t kMaxNodes = 1u << 24;   // the packed word's leftFirst field is 24 bits wide
 
+// The first `want` sibling pairs in breadth-first order from the root (pair 0 = root + the
+// unused node 1 stays first), the remaining pairs in their original relative (DFS) order;
+// interior leftFirst values renumbered.  Returns the number of leading pairs placed
+// breadth-first (<= want): the lane kernel's LDS treelet.
+uint32_t bfs_top_order(const Bvh &b, uint32_t want, std::vector<Node> &out) {
+    const uint32_t npairs = (b.nodes_used + 1) / 2;
+    std::vector<uint32_t> newof(npairs, UINT32_MAX), order;
+    order.reserve(npairs);
+    newof[0] = 0;
+    order.push_back(0);
+    std::vector<uint32_t> queue;
+    auto kids = [&](uint32_t node) {
+        const Node &nd = b.nodes[node];
+        if (nd.count == 0 && nd.leftFirst >= 2) queue.push_back(nd.leftFirst / 2);
+    };
+    kids(0);
+    for (size_t qi = 0; qi < queue.size() && order.size() < want; ++qi) {
+        const uint32_t p = queue[qi];
+        if (newof[p] != UINT32_MAX) continue;
+        newof[p] = (uint32_t)order.size();
+        order.push_back(p);
+        kids(2 * p);
+        kids(2 * p + 1);
+    }
+    const uint32_t placed = (uint32_t)order.size();
+    for (uint32_t p = 0; p < npairs; ++p)
+        if (newof[p] == UINT32_MAX) { newof[p] = (uint32_t)order.size(); order.push_back(p); }
+    out.assign(b.nodes.begin(), b.nodes.begin() + b.nodes_used);
+    for (uint32_t p = 0; p < npairs; ++p)
+        for (uint32_t c = 0; c < 2 && 2 * p + c < b.nodes_used; ++c) {
+            Node nd = b.nodes[2 * p + c];
+            if (nd.count == 0 && !(p == 0 && c == 1)) nd.leftFirst = 2 * newof[nd.leftFirst / 2];
+            out[2 * newof[p] + c] = nd;
+        }
+    return placed;
+}
+
 int validate_bvh(const Bvh &b, uint32_t n) {
     if (b.nodes_used < 2 || b.nodes_used > b.nodes.size()) return fail(RT_ERR_INVALID, "BVH node count out of range");
     std::vector<uint8_t> seen(n, 0);
@@ -276,10 +313,24 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (s->bvh.depth > 64) { delete s; return fail(RT_ERR_UNSUPPORTED, "BVH deeper than 64 (the reference's stack[64])"); }
     s->stack_depth = pick_stack(s->bvh.depth);
 
+    // ---- device node order: the reference's (DFS) order, or with RT_PT_TREELET the top pairs
+    // renumbered breadth-first so that the lane kernel's LDS copy of nodes [0, 2 T) holds the
+    // top of the tree (traversal order and arithmetic do not depend on where a node is stored)
+    uint32_t tl_pairs = 0;
+    if (const char *e = std::getenv("RT_PT_TREELET")) {
+        // LDS left beside the 1024-lane stacks (160 KB per CU, one workgroup)
+        const long budget = 160l * 1024 - (long)s->stack_depth * 1024 * 4 - 1024;
+        const long want = std::atol(e) > 1 ? std::atol(e) : budget / 64;
+        if (std::atoi(e) != 0 && budget >= 64 * 64) tl_pairs = (uint32_t)std::min<long>(want, budget / 64);
+    }
+    std::vector<Node> bfs_nodes;
+    if (tl_pairs) tl_pairs = bfs_top_order(s->bvh, tl_pairs, bfs_nodes);
+    const std::vector<Node> &dn = tl_pairs ? bfs_nodes : s->bvh.nodes;
+
     // ---- device node array: packed (leftFirst << 8 | count) word in b.z
     std::vector<float4> nodes(2 * (size_t)s->bvh.nodes_used);
     for (uint32_t i = 0; i < s->bvh.nodes_used; ++i) {
-        const Node &nd = s->bvh.nodes[i];
+        const Node &nd = dn[i];
         uint32_t word = (nd.leftFirst << 8) | nd.count;
         nodes[2 * i] = make_float4(nd.mn[0], nd.mn[1], nd.mn[2], nd.mx[0]);
         nodes[2 * i + 1] = make_float4(nd.mx[1], nd.mx[2], ubits(word), 0.0f);
@@ -288,7 +339,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     // (2k, 2k+1) at float4 4k: X = (mn.x, mn.x', mx.x, mx.x'), Y, Z alike, then the words
     std::vector<float4> pairs(nodes.size(), make_float4(0, 0, 0, 0));
     for (uint32_t k = 1; 2 * k + 1 < s->bvh.nodes_used; ++k) {
-        const Node &a = s->bvh.nodes[2 * k], &b = s->bvh.nodes[2 * k + 1];
+        const Node &a = dn[2 * k], &b = dn[2 * k + 1];
         const uint32_t wa = (a.leftFirst << 8) | a.count, wb = (b.leftFirst << 8) | b.count;
         pairs[4 * k + 0] = make_float4(a.mn[0], b.mn[0], a.mx[0], b.mx[0]);
         pairs[4 * k + 1] = make_float4(a.mn[1], b.mn[1], a.mx[1], b.mx[1]);
@@ -300,7 +351,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     std::vector<uint32_t> words(s->bvh.nodes_used, 0u);
     for (uint32_t k = 1; 2 * k + 1 < s->bvh.nodes_used; ++k)
         for (int c = 0; c < 3; ++c) pairs48[3 * k + c] = pairs[4 * k + c];
-    for (uint32_t i = 0; i < s->bvh.nodes_used; ++i) words[i] = (s->bvh.nodes[i].leftFirst << 8) | s->bvh.nodes[i].count;
+    for (uint32_t i = 0; i < s->bvh.nodes_used; ++i) words[i] = (dn[i].leftFirst << 8) | dn[i].count;
     // ---- leaf-order primitive records and per-id shading records; cubes and quads keep
     // their matrices and data in a side table (8 float4 each)
     static const float I16[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
@@ -476,8 +527,9 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         v.light_invr = 1.0f / L.v[3];
         v.light_area = 4.0f * kPI * v.light_r2;                        // Primitive.h:452
     }
-    const Node &root = s->bvh.nodes[0];
+    const Node &root = dn[0];
     v.root_word = (root.leftFirst << 8) | root.count;
+    v.tl_nodes = 2u * tl_pairs;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, s->device) == hipSuccess && prop.multiProcessorCount > 0)

@@ -601,3 +601,31 @@ def test_zero_seed_pixel_terminates_and_matches(rt, scenes, depth, spp):
     assert np.abs(r.accumulator() - acc).max() <= PIX_TOL
     assert np.array_equal(got, want)
     assert r.counters()["shadow"] == st["shadow"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recipe,spp,depth,tl", [("cfg5", 4, 10, "1"), ("cfg3", 2, 4, "1"), ("cfg5", 2, 6, "200"),
+                                                  ("teapotF", 2, 10, "1")])
+def test_treelet_lane_kernel_equals_default(rt, torch, monkeypatch, recipe, spp, depth, tl):
+    """RT_PT_TREELET: BFS-renumbered top pairs copied to LDS by a 1024-lane state machine.
+    At 1080p the bounce levels are large enough for the state machine (not the drain), so
+    this holds its frames, accumulators and ray counters to the default lane kernel's."""
+    W, H = 1920, 1080
+    monkeypatch.setenv("RT_PT_TREELET", "0")
+    s_a = rt.Scene.recipe(recipe)
+    monkeypatch.setenv("RT_PT_TREELET", tl)
+    s_b = rt.Scene.recipe(recipe)
+    ra, rb = rt.Renderer(s_a, W, H), rt.Renderer(s_b, W, H)
+    for f in range(2):
+        a = ra.tick_host(spp=spp, depth=depth, frame=f)
+        b = rb.tick_host(spp=spp, depth=depth, frame=f)
+        assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
+    assert np.array_equal(ra.accumulator(), rb.accumulator())
+    assert ra.counters() == rb.counters()
+    # the renumbered device tree answers the batched queries identically too
+    rays = random_rays(20000, 17)
+    ta, oa, ua, va = (x.cpu().numpy() for x in s_a.IntersectBVH(rays))
+    tb, ob, ub, vb = (x.cpu().numpy() for x in s_b.IntersectBVH(rays))
+    assert np.array_equal(oa, ob) and np.array_equal(ta.view(np.uint32), tb.view(np.uint32))
+    assert np.array_equal(s_a.IsOccluded(rays).cpu().numpy(), s_b.IsOccluded(rays).cpu().numpy())
+    assert np.array_equal(s_a.bvh()[0], s_b.bvh()[0])     # rt_scene_copy_bvh keeps the reference order

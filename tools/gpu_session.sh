@@ -25,7 +25,7 @@ for s in "$@"; do
             step bench_cfg4 300 python bench.py --config 4 --steps 30 --warmup 5 --no-cpu-baseline
             step bench_cfg5 300 python bench.py --config 5 --steps 10 --warmup 2 --no-cpu-baseline ;;
         profcfg)   # kernel trace + PMC passes of every config's bench run, summarised by tools/roofline.py
-            for c in 2 3 4 5; do
+            for c in ${PROF_CONFIGS:-2 3 4 5}; do
                 if [ $c = 2 ] || [ $c = 4 ]; then n=60; k="k_render<0, 1, false>"; else n=6; k="k_pt_lanes"; fi
                 b="python bench.py --config $c --steps $n --warmup 2 --no-cpu-baseline --ramp-seconds 0.3"
                 step prof_c$c 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pc$c/trace -o run --output-format csv -- $b

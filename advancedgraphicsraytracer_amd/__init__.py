@@ -31,6 +31,7 @@ MODE_PATH = 0
 MODE_WHITTED = 1
 MODE_PACKET = 2
 WALK_LANE, WALK_WAVE, WALK_AUTO = 0, 1, 2
+BVH_PLAIN, BVH_SBVH = 0, 1
 # renderer.h:9, renderer.h:13, renderer.cpp:105 (TracePacket's bounces: Trace's default depth)
 DEFAULT_DEPTH = {MODE_PATH: 10, MODE_WHITTED: 20, MODE_PACKET: 10}
 RECIPES = ("teapotF", "teapot", "mig16", "cfg3", "cfg5")
@@ -61,11 +62,12 @@ class SceneDesc(C.Structure):
                 ("sky_pixels", C.POINTER(C.c_uint32)), ("sky_width", C.c_uint32), ("sky_height", C.c_uint32),
                 ("bvh_nodes", C.c_void_p), ("bvh_num_nodes", C.c_uint32), ("bvh_indices", C.POINTER(C.c_uint32)),
                 ("device", C.c_int32), ("transforms", C.POINTER(C.c_float)),
-                ("textures", C.POINTER(Texture)), ("num_textures", C.c_uint32)]
+                ("textures", C.POINTER(Texture)), ("num_textures", C.c_uint32), ("bvh_kind", C.c_int32)]
 
 
 class SceneInfo(C.Structure):
-    _fields_ = [("num_prims", C.c_uint32), ("nodes_used", C.c_uint32), ("depth", C.c_uint32), ("max_leaf", C.c_uint32)]
+    _fields_ = [("num_prims", C.c_uint32), ("nodes_used", C.c_uint32), ("depth", C.c_uint32), ("max_leaf", C.c_uint32),
+                ("num_refs", C.c_uint32)]
 
 
 class Camera(C.Structure):
@@ -121,9 +123,12 @@ def lib():
                                 C.POINTER(u32)], C.c_int),
         "rt_bvh_build_host": ([C.POINTER(Prim), C.POINTER(C.c_float), u32, vp, C.POINTER(u32), C.POINTER(SceneInfo)],
                               C.c_int),
+        "rt_sbvh_build_host": ([C.POINTER(Prim), C.POINTER(C.c_float), u32, C.POINTER(vp), C.POINTER(C.POINTER(u32)),
+                                C.POINTER(SceneInfo)], C.c_int),
         "rt_image_load": ([C.c_char_p, C.POINTER(C.POINTER(u32)), C.POINTER(u32), C.POINTER(u32)], C.c_int),
         "rt_scene_create": ([C.POINTER(SceneDesc), C.POINTER(vp)], C.c_int),
         "rt_scene_create_recipe": ([C.c_char_p, C.c_char_p, i32, C.POINTER(vp)], C.c_int),
+        "rt_scene_create_recipe_ex": ([C.c_char_p, C.c_char_p, i32, i32, C.POINTER(vp)], C.c_int),
         "rt_scene_destroy": ([vp], C.c_int),
         "rt_scene_get_info": ([vp, C.POINTER(SceneInfo)], C.c_int),
         "rt_scene_set_camera_walk": ([vp, C.c_int], C.c_int),
@@ -288,8 +293,26 @@ def build_bvh_host(prims):
     return nodes[:info.nodes_used], idx, _info_dict(info)
 
 
+def build_sbvh_host(prims):
+    """The opt-in spatial-split BVH on the host: (nodes [n, 32] uint8, reference indices, info)."""
+    L = lib()
+    pa = (Prim * len(prims))(*prims)
+    T = _transforms(prims)
+    nodes, idx, info = C.c_void_p(), C.POINTER(C.c_uint32)(), SceneInfo()
+    _check(L.rt_sbvh_build_host(pa, T.ctypes.data_as(C.POINTER(C.c_float)) if T is not None else None, len(prims),
+                                C.byref(nodes), C.byref(idx), C.byref(info)))
+    try:
+        out_nodes = np.frombuffer(C.string_at(nodes, 32 * info.nodes_used), np.uint8).reshape(-1, 32).copy()
+        out_idx = np.ctypeslib.as_array(idx, shape=(info.num_refs,)).copy()
+    finally:
+        L.rt_free(nodes)
+        L.rt_free(C.cast(idx, C.c_void_p))
+    return out_nodes, out_idx, _info_dict(info)
+
+
 def _info_dict(info):
-    return {"num_prims": info.num_prims, "nodes_used": info.nodes_used, "depth": info.depth, "max_leaf": info.max_leaf}
+    return {"num_prims": info.num_prims, "nodes_used": info.nodes_used, "depth": info.depth, "max_leaf": info.max_leaf,
+            "num_refs": info.num_refs}
 
 
 def sphere(center, radius, material):
@@ -368,7 +391,8 @@ def _as_device_rays(rays, device):
 class Scene:
     """Scene (template/scene.h:37): primitives + materials + plain BVH, resident in HBM."""
 
-    def __init__(self, prims=None, materials=None, sky=None, bvh=None, device=0, textures=(), _handle=None):
+    def __init__(self, prims=None, materials=None, sky=None, bvh=None, device=0, textures=(), _handle=None,
+                 bvh_kind=BVH_PLAIN):
         """prims: Prim records (cube()/quad() carry their mat4 in .T); textures: uint32 [h, w]
         arrays of 0x00RRGGBB referenced by texture_material(index)."""
         self.L = lib()
@@ -383,6 +407,7 @@ class Scene:
         d.prims, d.num_prims = pa, len(prims)
         d.materials, d.num_materials = ma, len(materials)
         d.device = device
+        d.bvh_kind = bvh_kind
         keep = []
         if sky is not None:
             sky = np.ascontiguousarray(sky, np.uint32)
@@ -410,10 +435,11 @@ class Scene:
         _check(self.L.rt_scene_create(C.byref(d), C.byref(self.h)))
 
     @classmethod
-    def recipe(cls, name, mesh_dir=DATA_DIR, device=0):
-        """One of the SURVEY.md 8(d) benchmark scenes ("teapotF", "teapot", "mig16", "cfg3", "cfg5")."""
+    def recipe(cls, name, mesh_dir=DATA_DIR, device=0, bvh_kind=BVH_PLAIN):
+        """One of the SURVEY.md 8(d) benchmark scenes ("teapotF", "teapot", "mig16", "cfg3", "cfg5");
+        bvh_kind BVH_SBVH builds the opt-in spatial-split tree."""
         h = C.c_void_p()
-        _check(lib().rt_scene_create_recipe(name.encode(), os.fsencode(mesh_dir), device, C.byref(h)))
+        _check(lib().rt_scene_create_recipe_ex(name.encode(), os.fsencode(mesh_dir), device, bvh_kind, C.byref(h)))
         return cls(device=device, _handle=h)
 
     def close(self):
@@ -433,7 +459,7 @@ class Scene:
     def bvh(self):
         info = self.info
         nodes = np.zeros((info["nodes_used"], 32), np.uint8)
-        idx = np.zeros(info["num_prims"], np.uint32)
+        idx = np.zeros(info["num_refs"], np.uint32)
         _check(self.L.rt_scene_copy_bvh(self.h, nodes.ctypes.data_as(C.c_void_p),
                                         idx.ctypes.data_as(C.POINTER(C.c_uint32))))
         return nodes, idx

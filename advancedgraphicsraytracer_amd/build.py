@@ -13,7 +13,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librtamd.so")
 # the kernels are compiled twice (core / extension builds of rt_kernels.inc), in parallel
-SOURCES = ["rt_host.cpp", "rt_device.hip", "rt_kern_core.hip", "rt_kern_ext.hip", "rt_multi.cpp"]
+SOURCES = ["rt_host.cpp", "rt_device.hip", "rt_kern_core.hip", "rt_kern_ext.hip", "rt_multi.cpp", "rt_sbvh.cpp"]
 HEADERS = ["rt_math.h", "rt_internal.h", "rt_libm.h", "rt_dev_types.h", "rt_kernels.inc",
            os.path.join("..", "..", "include", "rt_amd.h")]
 

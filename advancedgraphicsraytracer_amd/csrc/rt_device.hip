@@ -274,6 +274,9 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     // word (leftFirst << 8 | count): trees with more than 2^24 nodes cannot be addressed
     if (d->bvh_nodes && d->bvh_num_nodes > kMaxNodes)
         return fail(RT_ERR_UNSUPPORTED, "prebuilt BVH with more than 2^24 nodes (24-bit child index)");
+    int32_t bvh_kind = d->bvh_kind;
+    if (const char *e = std::getenv("RT_BVH")) bvh_kind = std::strcmp(e, "sbvh") == 0 ? RT_BVH_SBVH : RT_BVH_PLAIN;
+    if (bvh_kind != RT_BVH_PLAIN && bvh_kind != RT_BVH_SBVH) return fail(RT_ERR_INVALID, "unknown bvh_kind");
     int rc = ensure_device(d->device);
     if (rc != RT_OK) return rc;
 
@@ -304,7 +307,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
             st.push_back({nd.leftFirst, dd + 1});
             st.push_back({nd.leftFirst + 1, dd + 1});
         }
-    } else if ((rc = build_bvh(d->prims, d->transforms, n, s->bvh)) != RT_OK) {
+    } else if ((rc = (bvh_kind == RT_BVH_SBVH ? build_sbvh : build_bvh)(d->prims, d->transforms, n, s->bvh)) != RT_OK) {
         delete s;
         return rc;
     }
@@ -355,7 +358,8 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     // ---- leaf-order primitive records and per-id shading records; cubes and quads keep
     // their matrices and data in a side table (8 float4 each)
     static const float I16[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-    std::vector<float4> prims(3 * (size_t)n), shade(2 * (size_t)n), xprims;
+    const uint32_t nrefs = (uint32_t)s->bvh.indices.size();   // leaf slots (an SBVH repeats primitives)
+    std::vector<float4> prims(3 * (size_t)nrefs), shade(2 * (size_t)n), xprims;
     std::vector<uint32_t> xindex(n, 0);
     for (uint32_t id = 0; id < n; ++id) {
         const rt_prim &p = d->prims[id];
@@ -400,7 +404,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         shade[2 * id] = s0;
         shade[2 * id + 1] = s1;
     }
-    for (uint32_t k = 0; k < n; ++k) {
+    for (uint32_t k = 0; k < nrefs; ++k) {
         const uint32_t id = s->bvh.indices[k];
         const rt_prim &p = d->prims[id];
         float4 *q = &prims[3 * (size_t)k];
@@ -1027,6 +1031,10 @@ int rt_scene_create(const rt_scene_desc *desc, rt_scene **out) {
 }
 
 int rt_scene_create_recipe(const char *name, const char *mesh_dir, int32_t device, rt_scene **out) {
+    return rt_scene_create_recipe_ex(name, mesh_dir, device, RT_BVH_PLAIN, out);
+}
+
+int rt_scene_create_recipe_ex(const char *name, const char *mesh_dir, int32_t device, int32_t bvh_kind, rt_scene **out) {
     if (!name || !mesh_dir || !out) return fail(RT_ERR_INVALID, "rt_scene_create_recipe: null argument");
     try {
         SceneSource src;
@@ -1038,6 +1046,7 @@ int rt_scene_create_recipe(const char *name, const char *mesh_dir, int32_t devic
         d.materials = src.materials.data();
         d.num_materials = (uint32_t)src.materials.size();
         d.device = device;
+        d.bvh_kind = bvh_kind;
         return scene_create(&d, out);
     } catch (const std::exception &e) {
         return fail(RT_ERR_INVALID, std::string("rt_scene_create_recipe: ") + e.what());
@@ -1055,6 +1064,7 @@ int rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
     info->nodes_used = s->bvh.nodes_used;
     info->depth = s->bvh.depth;
     info->max_leaf = s->bvh.max_leaf;
+    info->num_refs = (uint32_t)s->bvh.indices.size();
     return RT_OK;
 }
 
@@ -1071,7 +1081,7 @@ int rt_scene_set_camera_walk(rt_scene *s, int walk) {
 int rt_scene_copy_bvh(const rt_scene *s, void *nodes, uint32_t *indices) {
     if (!s || !nodes || !indices) return fail(RT_ERR_INVALID, "null argument");
     std::memcpy(nodes, s->bvh.nodes.data(), sizeof(Node) * s->bvh.nodes_used);
-    std::memcpy(indices, s->bvh.indices.data(), sizeof(uint32_t) * s->num_prims);
+    std::memcpy(indices, s->bvh.indices.data(), sizeof(uint32_t) * s->bvh.indices.size());
     return RT_OK;
 }
 

@@ -846,7 +846,27 @@ int rt_bvh_build_host(const rt_prim *prims, const float *transforms, uint32_t n,
     if (rc != RT_OK) return rc;
     std::memcpy(nodes, b.nodes.data(), sizeof(Node) * b.nodes.size());
     std::memcpy(indices, b.indices.data(), sizeof(uint32_t) * n);
-    if (info) { info->num_prims = n; info->nodes_used = b.nodes_used; info->depth = b.depth; info->max_leaf = b.max_leaf; }
+    if (info) { info->num_prims = n; info->nodes_used = b.nodes_used; info->depth = b.depth; info->max_leaf = b.max_leaf; info->num_refs = n; }
+    return RT_OK;
+}
+
+int rt_sbvh_build_host(const rt_prim *prims, const float *transforms, uint32_t n, void **nodes, uint32_t **indices,
+                       rt_scene_info *info) {
+    if (!prims || !nodes || !indices) return fail(RT_ERR_INVALID, "rt_sbvh_build_host: null argument");
+    *nodes = nullptr;
+    *indices = nullptr;
+    Bvh b;
+    int rc = build_sbvh(prims, transforms, n, b);
+    if (rc != RT_OK) return rc;
+    *nodes = std::malloc(sizeof(Node) * b.nodes_used);
+    *indices = static_cast<uint32_t *>(std::malloc(sizeof(uint32_t) * std::max<size_t>(1, b.indices.size())));
+    if (!*nodes || !*indices) return fail(RT_ERR_INVALID, "rt_sbvh_build_host: out of memory");
+    std::memcpy(*nodes, b.nodes.data(), sizeof(Node) * b.nodes_used);
+    std::memcpy(*indices, b.indices.data(), sizeof(uint32_t) * b.indices.size());
+    if (info) {
+        info->num_prims = n; info->nodes_used = b.nodes_used; info->depth = b.depth; info->max_leaf = b.max_leaf;
+        info->num_refs = (uint32_t)b.indices.size();
+    }
     return RT_OK;
 }
 

@@ -40,6 +40,8 @@ struct Bvh {
     uint32_t nodes_used = 0, depth = 0, max_leaf = 0;
 };
 int build_bvh(const rt_prim *prims, const float *transforms, uint32_t n, Bvh &out);
+// Spatial-split BVH (rt_sbvh.cpp): indices hold references (a primitive may repeat)
+int build_sbvh(const rt_prim *prims, const float *transforms, uint32_t n, Bvh &out);
 
 // frame size and device of a renderer (rt_multi.cpp)
 int renderer_geometry(const rt_renderer *r, uint32_t *W, uint32_t *H, int *device);

@@ -97,9 +97,17 @@ typedef struct {
      * RT_QUAD only; NULL = identity for all (the factories' default argument) */
     const float *transforms;
     const rt_texture *textures; uint32_t num_textures;
+    /* RT_BVH_PLAIN (0): the reference's plain binned-SAH BVH (template/scene.h:845-976), the
+     * parity tree; RT_BVH_SBVH: spatial splits (template/scene.h:521-840, built NaN-safe with a
+     * growing pool) -- closest hits equal the plain tree's except exact-distance ties.
+     * Ignored with a prebuilt BVH. */
+    int32_t bvh_kind;
 } rt_scene_desc;
+enum { RT_BVH_PLAIN = 0, RT_BVH_SBVH = 1 };
 
-typedef struct { uint32_t num_prims, nodes_used, depth, max_leaf; } rt_scene_info;
+/* num_refs = entries of the BVH's primitive-index array (= num_prims for the plain tree;
+ * more for an SBVH, whose leaves may share primitives) */
+typedef struct { uint32_t num_prims, nodes_used, depth, max_leaf, num_refs; } rt_scene_info;
 
 /* Ray / hit records of the batched entry points (Ray.h:7-32). */
 typedef struct { float ox, oy, oz, dx, dy, dz, tmax; } rt_ray;       /* 28 B */
@@ -150,6 +158,11 @@ int rt_recipe_describe(const char *name, const char *mesh_dir, rt_prim *prims, u
  * transforms as in rt_scene_desc (NULL = identity) */
 int rt_bvh_build_host(const rt_prim *prims, const float *transforms, uint32_t n, void *nodes, uint32_t *indices,
                       rt_scene_info *info);
+/* the opt-in spatial-split BVH (RT_BVH_SBVH) on the host: library-allocated nodes
+ * (info->nodes_used x 32 B) and primitive-index array (info->num_refs; primitives may
+ * repeat); free both with rt_free */
+int rt_sbvh_build_host(const rt_prim *prims, const float *transforms, uint32_t n, void **nodes, uint32_t **indices,
+                       rt_scene_info *info);
 /* Surface::LoadImage (template/template.cpp:1579-1601) for PNG files (8/16-bit grey,
  * grey+alpha, RGB, RGBA, palette; not interlaced): pixels = 0x00RRGGBB; free with rt_free. */
 int rt_image_load(const char *path, uint32_t **pixels, uint32_t *width, uint32_t *height);
@@ -158,6 +171,8 @@ int rt_image_load(const char *path, uint32_t **pixels, uint32_t *width, uint32_t
 int rt_scene_create(const rt_scene_desc *desc, rt_scene **out);
 /* the SURVEY.md 8(d) scenes: "teapotF", "teapot", "mig16", "cfg3", "cfg5" */
 int rt_scene_create_recipe(const char *name, const char *mesh_dir, int32_t device, rt_scene **out);
+/* the same with the BVH kind chosen (RT_BVH_PLAIN / RT_BVH_SBVH) */
+int rt_scene_create_recipe_ex(const char *name, const char *mesh_dir, int32_t device, int32_t bvh_kind, rt_scene **out);
 int rt_scene_destroy(rt_scene *s);
 int rt_scene_get_info(const rt_scene *s, rt_scene_info *info);
 /* How the primary+shadow frame kernel walks the BVH for camera rays (results identical):
@@ -173,7 +188,7 @@ int rt_scene_get_info(const rt_scene *s, rt_scene_info *info);
  * environment forces LANE / WAVE at scene creation. */
 enum { RT_WALK_LANE = 0, RT_WALK_WAVE = 1, RT_WALK_AUTO = 2 };
 int rt_scene_set_camera_walk(rt_scene *s, int walk);
-/* host copy of the BVH in use (nodes_used x 32 B, num_prims x u32) */
+/* host copy of the BVH in use (nodes_used x 32 B, num_refs x u32), in the reference's node order */
 int rt_scene_copy_bvh(const rt_scene *s, void *nodes, uint32_t *indices);
 
 /* Batched Scene::IntersectBVH (template/scene.h:285-320): rays_dev[n] -> hits_dev[n]. */

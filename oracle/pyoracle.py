@@ -54,7 +54,7 @@ def lib():
             getattr(L, n).restype = C.c_int
         L.or_scene_nodes.restype = vp
         L.or_scene_nodes.argtypes = [vp]
-        L.or_scene_set_bvh.argtypes = [vp, vp, C.c_int, C.POINTER(C.c_uint32)]
+        L.or_scene_set_bvh.argtypes = [vp, vp, C.c_int, C.POINTER(C.c_uint32), C.c_int]
         L.or_scene_set_bvh.restype = C.c_int
         L.or_scene_indices.restype = C.POINTER(C.c_uint32)
         L.or_scene_indices.argtypes = [vp]

@@ -694,13 +694,14 @@ int or_scene_build_bvh(or_scene *s) {   /* BuildBVH 845-853 with the 2N+1 pool o
     s->depth = max_depth(s, 0);
     return s->nodesUsed;
 }
-/* A prebuilt plain BVH (BVHNode.h:5-14 nodes + primitiveIndices) instead of BuildBVH: the
- * analytic known-answer tests fix the tree so that slab outcomes follow from the boxes alone. */
-int or_scene_set_bvh(or_scene *s, const void *nodes, int nodes_used, const uint32_t *idx) {
-    if (nodes_used < 2) return -1;
+/* A prebuilt BVH (BVHNode.h:5-14 nodes + primitiveIndices) instead of BuildBVH: the analytic
+ * known-answer tests fix the tree so that slab outcomes follow from the boxes alone, and the
+ * SBVH test runs the library's spatial-split tree (nidx references) through this traversal. */
+int or_scene_set_bvh(or_scene *s, const void *nodes, int nodes_used, const uint32_t *idx, int nidx) {
+    if (nodes_used < 2 || nidx < 1) return -1;
     free(s->idx); free(s->nodes);
-    s->idx = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(s->np > 0 ? s->np : 1));
-    memcpy(s->idx, idx, sizeof(uint32_t) * (size_t)s->np);
+    s->idx = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)nidx);   /* nidx > np: an SBVH's references */
+    memcpy(s->idx, idx, sizeof(uint32_t) * (size_t)nidx);
     s->nodes = (node *)calloc((size_t)nodes_used, sizeof(node));
     memcpy(s->nodes, nodes, sizeof(node) * (size_t)nodes_used);
     s->nodesUsed = nodes_used;

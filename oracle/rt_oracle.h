@@ -84,7 +84,7 @@ int or_scene_add_plane(or_scene *s, const float n[3], float d, int mat);
 int or_scene_add_triangle(or_scene *s, const float v0[3], const float v1[3], const float v2[3], int mat);
 int or_scene_add_mesh(or_scene *s, const float *verts, int nv, const int *tris, int nt, const float M[16], int mat);
 int or_scene_build_bvh(or_scene *s);
-int or_scene_set_bvh(or_scene *s, const void *nodes, int nodes_used, const uint32_t *idx);
+int or_scene_set_bvh(or_scene *s, const void *nodes, int nodes_used, const uint32_t *idx, int nidx);
 int or_scene_num_prims(const or_scene *s);
 int or_scene_nodes_used(const or_scene *s);
 int or_scene_depth(const or_scene *s);

@@ -36,7 +36,7 @@ def oracle_scene(rt, oracle, prims, mats, sky=None, textures=(), bvh=None):
     else:
         nodes, idx = np.ascontiguousarray(bvh[0], np.uint8), np.ascontiguousarray(bvh[1], np.uint32)
         assert L.or_scene_set_bvh(h, nodes.ctypes.data_as(C.c_void_p), len(nodes),
-                                  idx.ctypes.data_as(C.POINTER(C.c_uint32))) == len(nodes)
+                                  idx.ctypes.data_as(C.POINTER(C.c_uint32)), len(idx)) == len(nodes)
     o = oracle.Scene.__new__(oracle.Scene)
     o.L, o.h = L, h
     return o

@@ -629,3 +629,26 @@ def test_treelet_lane_kernel_equals_default(rt, torch, monkeypatch, recipe, spp,
     assert np.array_equal(oa, ob) and np.array_equal(ta.view(np.uint32), tb.view(np.uint32))
     assert np.array_equal(s_a.IsOccluded(rays).cpu().numpy(), s_b.IsOccluded(rays).cpu().numpy())
     assert np.array_equal(s_a.bvh()[0], s_b.bvh()[0])     # rt_scene_copy_bvh keeps the reference order
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recipe", ["teapotF", "mig16", "cfg3"])
+def test_sbvh_scene_matches_plain_oracle_except_ties(rt, scenes, recipe):
+    """The opt-in SBVH (RT_BVH_SBVH) on the GPU: closest-hit t bit-exact against the oracle's
+    plain BVH on camera and random rays, ids identical except exact-distance ties, occlusion
+    identical, and a primary+shadow frame that differs at most on tie pixels."""
+    g = rt.Scene.recipe(recipe, bvh_kind=rt.BVH_SBVH)
+    _, o = scenes(recipe)
+    info = g.info
+    assert info["num_refs"] > info["num_prims"]
+    W, H = 1920, 1080
+    rays = np.concatenate([o.camera_rays(W, H, strided_pixels(W, H, 13)), random_rays(30000, 23)])
+    t, obj, u, v = (x.cpu().numpy() for x in g.IntersectBVH(rays))
+    wt, wobj, _, _ = o.intersect(rays)
+    assert np.array_equal(t.view(np.uint32), wt.view(np.uint32))
+    assert (obj != wobj).mean() < 1e-3
+    short = rays.copy()
+    short[:, 6] = np.random.default_rng(5).uniform(0.0, 4.0, len(rays)).astype(np.float32)
+    assert np.array_equal(g.IsOccluded(short).cpu().numpy(), o.occluded(short).astype(bool))
+    got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, 480, 270, 1, 1)
+    assert (got != want).mean() < 1e-3

@@ -102,6 +102,7 @@ struct rt_comm {
     uint32_t *tiles[2] = {nullptr, nullptr};      // this rank's packed tiles (rank 0: unused)
     uint32_t *gathered[2] = {nullptr, nullptr};   // rank 0: world x cap, slot 0 rendered in place
     hipEvent_t ev_render[2] = {nullptr, nullptr}, ev_gather[2] = {nullptr, nullptr};
+    hipEvent_t ev_asm[2] = {nullptr, nullptr};   // rank 0, pipelined: frame assembled (comm stream)
     int slot = 0;
     int pending = -1;                      // slot whose gather is in flight (pipelined mode)
     uint64_t frames = 0;
@@ -248,6 +249,7 @@ int rt_comm_destroy(rt_comm *c) {
     for (int k = 0; k < 2; ++k) {
         if (c->ev_render[k]) (void)hipEventDestroy(c->ev_render[k]);
         if (c->ev_gather[k]) (void)hipEventDestroy(c->ev_gather[k]);
+        if (c->ev_asm[k]) (void)hipEventDestroy(c->ev_asm[k]);
     }
     for (auto &e : c->tev)
         for (auto &x : e) (void)hipEventDestroy(x);
@@ -289,27 +291,37 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
         return RT_OK;
     }
     // pipelined: this frame's gather runs on the communicator's stream while the caller's
-    // stream goes on (the next frame's render); the previous frame is completed here
+    // stream goes on (the next frame's render).  The previous frame is completed here: on rank
+    // 0 its unshuffle also runs on the communicator's stream, right behind its gather, so the
+    // render stream does not wait for it (only the render into its slot, one frame later, does)
     if (!c->comm_stream) {
         HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
         for (int j = 0; j < 2; ++j) {
             HIP_TRY(hipEventCreateWithFlags(&c->ev_render[j], hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&c->ev_gather[j], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_asm[j], hipEventDisableTiming));
         }
+    }
+    if (c->pending >= 0) {
+        // frame i-1: assembled after its gather (stream order on the comm stream); its buffers
+        // are rendered into again by the next call, which the render stream reaches only after
+        // this wait
+        const int j = c->pending;
+        if (c->rank == 0) {
+            if (!rgb8_dev) return fail(RT_ERR_INVALID, "rt_render_frame_multi: rank 0 needs an output frame");
+            if ((rc = assemble(c, r, j, rgb8_dev, c->comm_stream)) != RT_OK) return rc;
+            HIP_TRY(hipEventRecord(c->ev_asm[j], c->comm_stream));
+            HIP_TRY(hipStreamWaitEvent(st, c->ev_asm[j], 0));
+        } else {
+            HIP_TRY(hipStreamWaitEvent(st, c->ev_gather[j], 0));
+        }
+        c->frames += 1;
     }
     HIP_TRY(hipEventRecord(c->ev_render[k], st));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_render[k], 0));
     if ((rc = gather(c, k, c->comm_stream)) != RT_OK) return rc;
     HIP_TRY(hipEventRecord(c->ev_gather[k], c->comm_stream));
     if (tv) HIP_TRY(hipEventRecord((*tv)[2], c->comm_stream));
-    if (c->pending >= 0) {
-        // frame i-1: its gather must be done before it is assembled and before its buffers
-        // are rendered into again (the frame after this one)
-        const int j = c->pending;
-        HIP_TRY(hipStreamWaitEvent(st, c->ev_gather[j], 0));
-        if ((rc = assemble(c, r, j, rgb8_dev, st)) != RT_OK) return rc;
-        c->frames += 1;
-    }
     c->pending = k;
     c->slot = k ^ 1;
     return RT_OK;

@@ -216,12 +216,12 @@ def main():
     drain()
     torch.cuda.synchronize(device)
     c0 = rend.counters()
-    if sharded is not None:
-        sharded.set_timing(True)        # per-frame render / gather events from here on
-    # HIP events on the launch stream: at N = 1 one pair brackets the timed region (per-launch
-    # average = region / steps; no event packets between the frames), at N > 1 a pair around
-    # each shard render (the exchange runs between them)
-    per_step_events = world > 1 or args.per_step_events
+    # HIP events on the launch stream: one pair brackets the timed region (per-launch average =
+    # region / steps; no event packets between the frames).  At N > 1 the per-frame render /
+    # gather split comes from a separate instrumented pass after the timed region: timing
+    # events around every frame cost ~20 us per frame on the render stream (0.116 -> 0.138 ms
+    # per TEAPOT-F frame at world 1, profiles/r02/multi_overhead.json)
+    per_step_events = args.per_step_events
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps if per_step_events else 1)]
     if dist:
@@ -241,6 +241,12 @@ def main():
     t1 = time.perf_counter()
     c1 = rend.counters()
     elapsed = t1 - t0
+    if sharded is not None:   # untimed instrumented pass: per-frame render / exposed-gather times
+        sharded.set_timing(True)
+        for k in range(min(args.steps, 20)):
+            step(nf + args.steps + k)
+        drain()
+        torch.cuda.synchronize(device)
     frame_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) / (1 if per_step_events else args.steps)
     primary = c1["primary"] - c0["primary"]
     shadow = c1["shadow"] - c0["shadow"]

@@ -63,6 +63,44 @@ def main():
     with open(os.path.join(HERE, "frames.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     print(json.dumps(out, indent=1))
+    # 4. path-traced radiance of strided 1080p pixel subsets: Renderer::Trace
+    #    averaged over the frame's samples = the accumulator after frame 0
+    pt = {}
+    for recipe, spp, depth, stride in PT_SUBSETS:
+        sc = pyoracle.Scene(recipe, DATA_DIR)
+        px = np.arange(0, 1920 * 1080, stride, dtype=np.int32)
+        rgb, _ = sc.trace_pixels(1920, 1080, px, spp=spp, depth=depth, frame=0)
+        pt[f"{recipe}_spp{spp}_d{depth}_pixels"] = px
+        pt[f"{recipe}_spp{spp}_d{depth}_rgb"] = rgb
+    np.savez_compressed(os.path.join(HERE, "pt_subsets.npz"), **pt)
+    # 5. geometry digests: the recipes' primitive records after the OBJ
+    #    load (library) and the plain BVH (nodes with the unused slot 1 zeroed + indices, oracle)
+    geo = {}
+    for recipe in ("teapotF", "cfg3", "cfg5", "mig16"):
+        prims, _ = rt.recipe_describe(recipe)
+        sc = pyoracle.Scene(recipe, DATA_DIR)
+        nodes = sc.nodes().copy()
+        nodes[1] = 0
+        geo[recipe] = {"prims": len(prims), "prims_sha256": prims_digest(prims), "nodes_used": int(sc.nodes_used),
+                       "depth": int(sc.depth), "bvh_sha256": bvh_digest(nodes, sc.indices())}
+    with open(os.path.join(HERE, "geometry.json"), "w") as f:
+        json.dump(geo, f, indent=1, sort_keys=True)
+    print(json.dumps(geo, indent=1))
+
+
+# (recipe, spp, Trace depth, pixel stride) at 1920x1080, frame 0: the BASELINE path-tracing configs
+PT_SUBSETS = (("teapotF", 1, 10, 61), ("cfg3", 4, 4, 241), ("cfg5", 16, 10, 997))
+
+
+def prims_digest(prims):
+    import hashlib
+    return hashlib.sha256(b"".join(bytes(p) for p in prims)).hexdigest()
+
+
+def bvh_digest(nodes, indices):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(nodes, np.uint8).tobytes()
+                          + np.ascontiguousarray(indices, np.uint32).tobytes()).hexdigest()
 
 
 if __name__ == "__main__":

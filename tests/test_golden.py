@@ -129,3 +129,70 @@ def test_gpu_matches_prim_kat(rt):
     assert np.array_equal(occ, g["occluded"].astype(bool))
     hh = s.intersect_host(g["rays"])
     assert np.array_equal(hh["obj"], g["obj"])
+
+
+# ---- path-traced radiance subsets and geometry digests
+def load_pt():
+    return np.load(os.path.join(GOLD, "pt_subsets.npz"))
+
+
+def geometry():
+    with open(os.path.join(GOLD, "geometry.json")) as f:
+        return json.load(f)
+
+
+PT_KEYS = ["teapotF_spp1_d10", "cfg3_spp4_d4", "cfg5_spp16_d10"]
+
+
+def parse_pt(key):
+    recipe, spp, depth = key.split("_")
+    return recipe, int(spp[3:]), int(depth[1:])
+
+
+@pytest.mark.parametrize("recipe", ["teapotF", "cfg3", "cfg5", "mig16"])
+def test_geometry_digests(rt, oracle, recipe):
+    """The recipe's primitive records after the OBJ load, and the plain BVH (library host build
+    and oracle) hash to the committed digests."""
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_fixtures import bvh_digest, prims_digest
+    want = geometry()[recipe]
+    prims, _ = rt.recipe_describe(recipe)
+    assert len(prims) == want["prims"] and prims_digest(prims) == want["prims_sha256"]
+    nodes, idx, info = rt.build_bvh_host(prims)
+    nodes = nodes.copy()
+    nodes[1] = 0
+    assert info["nodes_used"] == want["nodes_used"] and info["depth"] == want["depth"]
+    assert bvh_digest(nodes[:want["nodes_used"]], idx) == want["bvh_sha256"]
+    o = oracle.Scene(recipe, rt.DATA_DIR)
+    on = o.nodes().copy()
+    on[1] = 0
+    assert bvh_digest(on, o.indices()) == want["bvh_sha256"]
+
+
+@pytest.mark.parametrize("key", PT_KEYS)
+def test_oracle_reproduces_pt_subsets(oracle, rt, key):
+    recipe, spp, depth = parse_pt(key)
+    g = load_pt()
+    px = g[key + "_pixels"]
+    s = oracle.Scene(recipe, rt.DATA_DIR)
+    rgb, _ = s.trace_pixels(1920, 1080, px, spp=spp, depth=depth, frame=0)
+    assert np.array_equal(rgb.view(np.uint32), g[key + "_rgb"].view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", PT_KEYS)
+def test_gpu_matches_golden_pt_subsets(rt, key):
+    """Full 1920x1080 frame 0 on the GPU (wavefront path tracer): the accumulator at the subset's
+    pixels equals the committed Renderer::Trace radiance bit for bit (the first frame's running
+    average is the frame's sample mean itself)."""
+    recipe, spp, depth = parse_pt(key)
+    g = load_pt()
+    px, want = g[key + "_pixels"], g[key + "_rgb"]
+    r = rt.Renderer(rt.Scene.recipe(recipe), 1920, 1080)
+    r.tick_host(spp=spp, depth=depth, frame=0, reset=True)
+    acc = r.accumulator()
+    got = acc[px, :3]
+    bad = np.flatnonzero((got.view(np.uint32) != want.view(np.uint32)).any(axis=1))
+    assert bad.size == 0, f"{bad.size} of {px.size} pixels differ, first {px[bad[:5]]}"
+    assert np.array_equal(acc[px, 3], np.ones(px.size, np.float32))

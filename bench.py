@@ -136,6 +136,33 @@ def cpu_baseline(args, spp):
     return out
 
 
+def companion_rate(scene, W, H, spp, depth, stream, device, warm=30, frames=300):
+    """The same workload at another frame size on a renderer of its own (BASELINE.json's
+    metric is quoted at 1280x720 and 1920x1080): warm-up frames (camera-walk and tile-order
+    tuning), then `frames` timed frames between two stream events and a wall clock."""
+    r = rt.Renderer(scene, W, H)
+    out = torch.zeros(W * H, dtype=torch.int32, device=f"cuda:{device}")
+    sptr = stream.cuda_stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        for i in range(warm):
+            r.Tick(out, spp=spp, depth=depth, frame=i, stream=sptr)
+        torch.cuda.synchronize(device)
+        c0 = r.counters()
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for i in range(frames):
+            r.Tick(out, spp=spp, depth=depth, frame=warm + i, stream=sptr)
+        e1.record(stream)
+        torch.cuda.synchronize(device)
+        wall = time.perf_counter() - t0
+    c1 = r.counters()
+    rays = sum(c1[k] - c0[k] for k in ("primary", "shadow", "bounce"))
+    return {"width": W, "height": H, "spp": spp, "depth": depth, "frames": frames,
+            "ms_per_frame": round(wall / frames * 1e3, 4), "frame_ms_events": round(e0.elapsed_time(e1) / frames, 4),
+            "mrays_s": round(rays / wall / 1e6, 3), "fps": round(frames / wall, 3)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -271,6 +298,9 @@ def main():
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     tot_rays, tot_primary, tot_shadow, tot_bounce = local_rays.tolist()
     wall = t_max.item()
+    companion = None
+    if world == 1 and args.depth == 1 and (W, H) == (1920, 1080):   # the metric's other frame size
+        companion = companion_rate(scene, 1280, 720, spp, args.depth, stream, device)
 
     if rank == 0:
         cfg = CONFIGS[args.config]
@@ -317,6 +347,8 @@ def main():
         }
         if multi:
             line["multi_gpu"] = multi
+        if companion:
+            line["at_720p"] = companion
         if world == 1 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(args, spp)

@@ -71,6 +71,8 @@ struct rt_scene {
                                     // waves (RT_SPLIT_HEAVY = count; -1: ntiles / 32)
     uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per renderer: 12 GB of the 288 GB HBM
                                               // holds all 16 spp of a 1080p depth-10 frame
+    bool pt_pipeline = true;        // sample batches alternate path-state slots and streams
+                                    // (RT_PT_PIPELINE=0: one slot, the caller's stream)
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
     void *d_xprims = nullptr, *d_tex = nullptr, *d_pairs = nullptr, *d_pairs48 = nullptr, *d_words = nullptr;
     void *d_scratch = nullptr;  // staging for the host-pointer batched calls
@@ -102,9 +104,17 @@ struct rt_renderer {
     int tune = 0;
     bool wave = false;
     hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
-    // wavefront path tracer (PathArgs): one allocation, grown on demand
-    void *d_pt = nullptr;
-    size_t pt_bytes = 0;
+    // wavefront path tracer (PathArgs): two path-state slots, grown on demand.  Sample batches
+    // alternate between them and between the renderer's two path streams, so one batch's level 0
+    // fills the CUs that the previous batch's thinning bounce levels leave idle; only the
+    // finishing pass (running sum, accumulator, RGB8) is ordered -- after the caller's stream
+    // at the frame's start and after the previous batch's finish
+    void *d_pt[2] = {nullptr, nullptr};
+    size_t pt_bytes[2] = {0, 0};
+    float4 *d_sum = nullptr;        // the frame's per-pixel sample sum across batches
+    hipStream_t pt_stream[2] = {nullptr, nullptr};
+    hipEvent_t pt_fin[2] = {nullptr, nullptr}, pt_entry = nullptr;
+    int pt_slot = 0, pt_last = -1;
     // per-sample values of sample-split frames (FrameArgs::samples)
     void *d_samples = nullptr;
     size_t samples_bytes = 0;
@@ -571,6 +581,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     // 0.377 -> 0.441 ms, 720p neutral) -- profiles/r02/ab_xcd_*.json.  RT_XCD_ORDER=0/1 forces it.
     s->xcd_order = (size_t)s->bvh.nodes_used * 32u + (size_t)n * 48u > (4u << 20);
     if (const char *e = std::getenv("RT_XCD_ORDER")) s->xcd_order = std::atoi(e) != 0;
+    if (const char *e = std::getenv("RT_PT_PIPELINE")) s->pt_pipeline = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
@@ -630,9 +641,10 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     // camera rays of level 0 take the wave-coherent walk when the scene forces it, or when
     // the renderer's primary+shadow frames timed it faster (RT_WALK_AUTO)
     view.wave_primary = !s->has_cubes && (s->walk == RT_WALK_WAVE || (s->walk == RT_WALK_AUTO && r->tune == 4 && r->wave));
+    const bool pipe = s->pt_pipeline;
     const uint64_t npix = (uint64_t)F.ntiles_local * 64u;
     const uint64_t per_path = 32u + 16u + 8u + (uint64_t)(F.depth - 1) * 32u;
-    const uint64_t budget = s->pt_mem_bytes;
+    const uint64_t budget = pipe ? s->pt_mem_bytes / 2 : s->pt_mem_bytes;   // per slot
     uint64_t batch = std::max<uint64_t>(1, budget / (per_path * npix));
     batch = std::min<uint64_t>(batch, F.spp);
     if (batch * npix > 0xffffffffull / 2) batch = std::max<uint64_t>(1, (0xffffffffull / 2) / npix);
@@ -642,56 +654,85 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     const uint64_t seg_cap = ((np / 64u + kQueueSegs - 1) / kQueueSegs + 1) * 64u;
     const size_t qbytes = (size_t)seg_cap * kQueueSegs * 4u;
     const size_t cbytes = (size_t)(F.depth + 1) * (2u * kQueueSegs) * 64u;   // queue counts + head counters
-    const size_t need = (size_t)(np * (per_path - 8u) + 2 * qbytes + npix * 16u + cbytes + 4096u);
-    if (need > r->pt_bytes) {
-        if (r->d_pt) HIP_TRY(hipFree(r->d_pt));
-        r->d_pt = nullptr;
-        r->pt_bytes = 0;
-        HIP_TRY(hipMalloc(&r->d_pt, need));
-        r->pt_bytes = need;
+    const size_t need = (size_t)(np * (per_path - 8u) + 2 * qbytes + cbytes + 4096u);
+    if (!r->d_sum) {   // one float4 per pixel of the whole frame (a shard uses its first npix)
+        const size_t tiles = (size_t)((r->W + 7) / 8) * ((r->H + 7) / 8);
+        HIP_TRY(hipMalloc(&r->d_sum, tiles * 64u * sizeof(float4)));
     }
-    char *b = static_cast<char *>(r->d_pt);
-    auto take = [&](size_t bytes) { char *q = b; b += (bytes + 255u) & ~(size_t)255u; return q; };
-    PathArgs P{};
-    P.state = reinterpret_cast<float4 *>(take(np * 32u));
-    P.result = reinterpret_cast<float4 *>(take(np * 16u));
-    uint32_t *q0 = reinterpret_cast<uint32_t *>(take(qbytes));
-    uint32_t *q1 = reinterpret_cast<uint32_t *>(take(qbytes));
-    P.sum = reinterpret_cast<float4 *>(take(npix * 16u));
-    P.qcount = reinterpret_cast<uint32_t *>(take(cbytes));
-    P.seg_cap = (uint32_t)seg_cap;
-    P.qhead = P.qcount + (size_t)(F.depth + 1) * kQueueSegs * 16u;
-    P.dynamic = s->pt_dynamic ? 1 : 0;
-    P.rec = reinterpret_cast<float4 *>(take((size_t)(F.depth - 1) * np * 32u));
+    if (pipe && !r->pt_stream[0]) {
+        for (int k = 0; k < 2; ++k) {
+            HIP_TRY(hipStreamCreateWithFlags(&r->pt_stream[k], hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&r->pt_fin[k], hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventCreateWithFlags(&r->pt_entry, hipEventDisableTiming));
+    }
+    // the caller's work before this frame (its accumulator / output use, the previous frame's
+    // finish) precedes the finishing passes only: the bounce levels touch renderer-private memory
+    if (pipe) HIP_TRY(hipEventRecord(r->pt_entry, st));
     const size_t lds = stack_bytes(s);
     // levels are compacted level by level until one is small enough to drain (k_pt_level)
     const uint32_t drain_level = s->pt_drain_level;
-    P.drain_level = drain_level;
-    P.drain_below = 0;
     for (uint32_t s0 = 0; s0 < F.spp; s0 += (uint32_t)batch) {
+        const int k = pipe ? r->pt_slot : 0;
+        if (pipe) r->pt_slot ^= 1;
+        hipStream_t X = pipe ? r->pt_stream[k] : st;
+        if (need > r->pt_bytes[k]) {
+            HIP_TRY(hipStreamSynchronize(X));   // the slot's previous batch is done with it
+            if (r->d_pt[k]) HIP_TRY(hipFree(r->d_pt[k]));
+            r->d_pt[k] = nullptr;
+            r->pt_bytes[k] = 0;
+            HIP_TRY(hipMalloc(&r->d_pt[k], need));
+            r->pt_bytes[k] = need;
+        }
+        char *b = static_cast<char *>(r->d_pt[k]);
+        auto take = [&](size_t bytes) { char *q = b; b += (bytes + 255u) & ~(size_t)255u; return q; };
+        PathArgs P{};
+        P.state = reinterpret_cast<float4 *>(take(np * 32u));
+        P.result = reinterpret_cast<float4 *>(take(np * 16u));
+        uint32_t *q0 = reinterpret_cast<uint32_t *>(take(qbytes));
+        uint32_t *q1 = reinterpret_cast<uint32_t *>(take(qbytes));
+        P.qcount = reinterpret_cast<uint32_t *>(take(cbytes));
+        P.seg_cap = (uint32_t)seg_cap;
+        P.qhead = P.qcount + (size_t)(F.depth + 1) * kQueueSegs * 16u;
+        P.dynamic = s->pt_dynamic ? 1 : 0;
+        P.rec = reinterpret_cast<float4 *>(take((size_t)(F.depth - 1) * np * 32u));
+        P.sum = r->d_sum;
+        P.drain_level = drain_level;
+        P.drain_below = 0;
         P.s0 = s0;
         P.batch_spp = std::min<uint32_t>((uint32_t)batch, F.spp - s0);
         P.npaths = (uint32_t)(P.batch_spp * npix);
-        HIP_TRY(hipMemsetAsync(P.qcount, 0, cbytes, st));
+        HIP_TRY(hipMemsetAsync(P.qcount, 0, cbytes, X));
         for (uint32_t level = 0; level < F.depth; ++level) {
             P.level = level;
             P.queue_in = (level & 1u) ? q1 : q0;
             P.queue_out = (level & 1u) ? q0 : q1;
             int resident = 0;
             if (level > 0 && s->pt_lanes) {             // incoherent levels: the lane state machine
-                if (s->ext) kext::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, st);
-                else kcore::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, st);
+                if (s->ext) kext::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, X);
+                else kcore::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, X);
             } else {
-                resident = s->ext ? kext::launch_pt_level(view, F, P, tex, lds, s->num_cus, st)
-                                  : kcore::launch_pt_level(view, F, P, tex, lds, s->num_cus, st);
+                resident = s->ext ? kext::launch_pt_level(view, F, P, tex, lds, s->num_cus, X)
+                                  : kcore::launch_pt_level(view, F, P, tex, lds, s->num_cus, X);
             }
             if (level >= drain_level) break;           // that launch finished every remaining level
             if (level == 0) P.drain_below = (uint32_t)std::min<double>(4e9, s->pt_drain_rounds * resident);
         }
+        // the finishing pass: in sample order after the previous batch's (the running sum), and
+        // after the caller's earlier work (the accumulator and output)
+        if (pipe) {
+            HIP_TRY(hipStreamWaitEvent(X, r->pt_entry, 0));
+            if (r->pt_last >= 0 && r->pt_last != k) HIP_TRY(hipStreamWaitEvent(X, r->pt_fin[r->pt_last], 0));
+        }
         const bool last = s0 + P.batch_spp >= F.spp;
-        if (s->ext) kext::launch_pt_finish(F, P, last, st);
-        else kcore::launch_pt_finish(F, P, last, st);
+        if (s->ext) kext::launch_pt_finish(F, P, last, X);
+        else kcore::launch_pt_finish(F, P, last, X);
+        if (pipe) {
+            HIP_TRY(hipEventRecord(r->pt_fin[k], X));
+            r->pt_last = k;
+        }
     }
+    if (pipe) HIP_TRY(hipStreamWaitEvent(st, r->pt_fin[r->pt_last], 0));   // the frame, in the caller's order
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }
@@ -1236,7 +1277,13 @@ int rt_renderer_destroy(rt_renderer *r) {
     (void)hipFree(r->d_acc);
     (void)hipFree(r->d_counters);
     if (r->d_rgb) (void)hipFree(r->d_rgb);
-    if (r->d_pt) (void)hipFree(r->d_pt);
+    for (int k = 0; k < 2; ++k) {
+        if (r->d_pt[k]) (void)hipFree(r->d_pt[k]);
+        if (r->pt_stream[k]) (void)hipStreamDestroy(r->pt_stream[k]);
+        if (r->pt_fin[k]) (void)hipEventDestroy(r->pt_fin[k]);
+    }
+    if (r->pt_entry) (void)hipEventDestroy(r->pt_entry);
+    if (r->d_sum) (void)hipFree(r->d_sum);
     if (r->d_samples) (void)hipFree(r->d_samples);
     if (r->d_order) (void)hipFree(r->d_order);
     if (r->d_cost) (void)hipFree(r->d_cost);

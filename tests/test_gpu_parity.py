@@ -467,6 +467,39 @@ def test_wavefront_equals_one_kernel_path_tracer(rt, torch, monkeypatch, recipe,
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("recipe,W,H,mem", [("cfg3", 200, 120, "3"), ("cfg5", 96, 64, "12288")])
+def test_pipelined_batches_equal_serial(rt, torch, monkeypatch, recipe, W, H, mem):
+    """Sample batches alternating two path-state slots and streams (the default) against the
+    one-slot path on the caller's stream: frames submitted back to back with no host sync in
+    between (the next frame's bounce levels overlap this frame's tail), several batches per
+    frame (3 MB of path state) or one, primary+shadow frames and a reset interleaved -- every
+    frame, the accumulator and the ray counters bit for bit."""
+    monkeypatch.setenv("RT_PT_MEM_MB", mem)
+    monkeypatch.setenv("RT_PT_PIPELINE", "0")
+    s0 = rt.Scene.recipe(recipe)
+    monkeypatch.setenv("RT_PT_PIPELINE", "1")
+    s1 = rt.Scene.recipe(recipe)
+    r0, r1 = rt.Renderer(s0, W, H), rt.Renderer(s1, W, H)
+    plan = [(4, 4, False), (4, 4, False), (1, 1, False), (8, 6, False), (2, 10, True), (4, 4, False)]
+    st = torch.cuda.Stream()
+    outs = []
+    with torch.cuda.stream(st):
+        for r in (r0, r1):
+            frames = []
+            for f, (spp, depth, reset) in enumerate(plan):
+                o = torch.zeros(W * H, dtype=torch.int32, device="cuda:0")
+                r.Tick(o, spp=spp, depth=depth, frame=f, reset=reset, stream=st.cuda_stream)
+                frames.append(o)
+            outs.append(frames)
+    torch.cuda.synchronize()
+    for f in range(len(plan)):
+        a, b = outs[0][f].cpu().numpy(), outs[1][f].cpu().numpy()
+        assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
+    assert np.array_equal(r0.accumulator(), r1.accumulator())
+    assert r0.counters() == r1.counters()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("recipe,W,H,spp,depth,mode,shards", [
     ("teapotF", 200, 120, 4, 1, 0, 1),      # primary+shadow, LDS kernel
     ("mig16", 160, 96, 3, 1, 0, 1),         # global-node kernel (wave walk AUTO)

@@ -69,8 +69,8 @@ struct rt_scene {
                                     // one compact screen region of 1/8 of the frame's cost (L2 locality)
     int32_t heavy_split = -1;       // primary+shadow frames: the costliest tiles run as two half-tile
                                     // waves (RT_SPLIT_HEAVY = count; -1: ntiles / 32)
-    uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per renderer: 12 GB of the 288 GB HBM
-                                              // holds all 16 spp of a 1080p depth-10 frame
+    uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per slot (two when pipelined): 12 GB
+                                              // of the 288 GB HBM holds all 16 spp of a 1080p depth-10 frame
     bool pt_pipeline = true;        // sample batches alternate path-state slots and streams
                                     // (RT_PT_PIPELINE=0: one slot, the caller's stream)
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
@@ -104,17 +104,24 @@ struct rt_renderer {
     int tune = 0;
     bool wave = false;
     hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
-    // wavefront path tracer (PathArgs): two path-state slots, grown on demand.  Sample batches
-    // alternate between them and between the renderer's two path streams, so one batch's level 0
-    // fills the CUs that the previous batch's thinning bounce levels leave idle; only the
-    // finishing pass (running sum, accumulator, RGB8) is ordered -- after the caller's stream
-    // at the frame's start and after the previous batch's finish
+    // wavefront path tracer (PathArgs): two path-state slots (state, records, queues), grown on
+    // demand, each owned by one of the renderer's two path streams.  Sample batches alternate
+    // between them, so one batch's (or the next frame's) level 0 fills the CUs that the other
+    // batch's thinning bounce levels leave idle.  The per-sample radiance goes to a frame-level
+    // buffer (two, by frame parity); one finishing pass per frame on the caller's stream sums
+    // it in sample order after every batch's levels (accumulator, RGB8).  d_pt[0] / the
+    // caller's stream alone when pipelining is off or the results do not fit.
     void *d_pt[2] = {nullptr, nullptr};
     size_t pt_bytes[2] = {0, 0};
-    float4 *d_sum = nullptr;        // the frame's per-pixel sample sum across batches
+    float4 *d_res[2] = {nullptr, nullptr};   // [sample][pixel] radiance of a frame, by frame parity
+    size_t res_bytes[2] = {0, 0};
+    float4 *d_sum = nullptr;        // the running sample sum across batches (serial path)
     hipStream_t pt_stream[2] = {nullptr, nullptr};
-    hipEvent_t pt_fin[2] = {nullptr, nullptr}, pt_entry = nullptr;
-    int pt_slot = 0, pt_last = -1;
+    hipEvent_t pt_lv[2] = {nullptr, nullptr};    // a path stream's levels of this frame are done
+    hipEvent_t pt_fin[2] = {nullptr, nullptr};   // the finish that read d_res[parity] is done
+    bool pt_fin_set[2] = {false, false};
+    int pt_slot = 0, pt_parity = 0;
+    bool pt_serial_last = false;    // the last path-traced frame ran the serial path
     // per-sample values of sample-split frames (FrameArgs::samples)
     void *d_samples = nullptr;
     size_t samples_bytes = 0;
@@ -641,10 +648,16 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     // camera rays of level 0 take the wave-coherent walk when the scene forces it, or when
     // the renderer's primary+shadow frames timed it faster (RT_WALK_AUTO)
     view.wave_primary = !s->has_cubes && (s->walk == RT_WALK_WAVE || (s->walk == RT_WALK_AUTO && r->tune == 4 && r->wave));
-    const bool pipe = s->pt_pipeline;
     const uint64_t npix = (uint64_t)F.ntiles_local * 64u;
+    // pipelined: per-sample results of the whole frame in a frame-level buffer (two by frame
+    // parity, up to 2 GB each); the serial path keeps them per batch with a running sum
+    const uint64_t res_need = (uint64_t)F.spp * npix * 16u;
+    const bool pipe = s->pt_pipeline && res_need <= (2ull << 30);
     const uint64_t per_path = 32u + 16u + 8u + (uint64_t)(F.depth - 1) * 32u;
-    const uint64_t budget = pipe ? s->pt_mem_bytes / 2 : s->pt_mem_bytes;   // per slot
+    // per slot: two slots of up to RT_PT_MEM_MB each when pipelined (fewer, larger batches and
+    // frame-to-frame overlap beat more batches: CFG5-sub 8.85 ms with half the budget per slot
+    // -- two batches a frame -- vs 8.51 ms with one batch a frame, profiles/r02/bench_pipe_*)
+    const uint64_t budget = s->pt_mem_bytes;
     uint64_t batch = std::max<uint64_t>(1, budget / (per_path * npix));
     batch = std::min<uint64_t>(batch, F.spp);
     if (batch * npix > 0xffffffffull / 2) batch = std::max<uint64_t>(1, (0xffffffffull / 2) / npix);
@@ -659,16 +672,32 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         const size_t tiles = (size_t)((r->W + 7) / 8) * ((r->H + 7) / 8);
         HIP_TRY(hipMalloc(&r->d_sum, tiles * 64u * sizeof(float4)));
     }
-    if (pipe && !r->pt_stream[0]) {
-        for (int k = 0; k < 2; ++k) {
-            HIP_TRY(hipStreamCreateWithFlags(&r->pt_stream[k], hipStreamNonBlocking));
-            HIP_TRY(hipEventCreateWithFlags(&r->pt_fin[k], hipEventDisableTiming));
+    int par = 0;
+    // slot 0 was last written on the caller's stream (a serial frame): that work is done before
+    // a path stream takes the slot over (a rare switch: frames whose results exceed the buffer)
+    if (pipe && r->pt_serial_last) HIP_TRY(hipStreamSynchronize(st));
+    r->pt_serial_last = !pipe;
+    if (pipe) {
+        if (!r->pt_stream[0]) {
+            for (int k = 0; k < 2; ++k) {
+                HIP_TRY(hipStreamCreateWithFlags(&r->pt_stream[k], hipStreamNonBlocking));
+                HIP_TRY(hipEventCreateWithFlags(&r->pt_lv[k], hipEventDisableTiming));
+                HIP_TRY(hipEventCreateWithFlags(&r->pt_fin[k], hipEventDisableTiming));
+            }
         }
-        HIP_TRY(hipEventCreateWithFlags(&r->pt_entry, hipEventDisableTiming));
+        par = r->pt_parity;
+        r->pt_parity ^= 1;
+        if (res_need > r->res_bytes[par]) {
+            HIP_TRY(hipDeviceSynchronize());   // every pending use of the old buffer
+            if (r->d_res[par]) HIP_TRY(hipFree(r->d_res[par]));
+            r->d_res[par] = nullptr;
+            r->res_bytes[par] = 0;
+            r->pt_fin_set[par] = false;
+            HIP_TRY(hipMalloc(&r->d_res[par], res_need));
+            r->res_bytes[par] = res_need;
+        }
     }
-    // the caller's work before this frame (its accumulator / output use, the previous frame's
-    // finish) precedes the finishing passes only: the bounce levels touch renderer-private memory
-    if (pipe) HIP_TRY(hipEventRecord(r->pt_entry, st));
+    bool used[2] = {false, false};
     const size_t lds = stack_bytes(s);
     // levels are compacted level by level until one is small enough to drain (k_pt_level)
     const uint32_t drain_level = s->pt_drain_level;
@@ -676,19 +705,22 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         const int k = pipe ? r->pt_slot : 0;
         if (pipe) r->pt_slot ^= 1;
         hipStream_t X = pipe ? r->pt_stream[k] : st;
-        if (need > r->pt_bytes[k]) {
+        const size_t slot_need = need + (pipe ? 0 : (size_t)np * 16u + 256u);   // serial: + the results
+        if (slot_need > r->pt_bytes[k]) {
             HIP_TRY(hipStreamSynchronize(X));   // the slot's previous batch is done with it
             if (r->d_pt[k]) HIP_TRY(hipFree(r->d_pt[k]));
             r->d_pt[k] = nullptr;
             r->pt_bytes[k] = 0;
-            HIP_TRY(hipMalloc(&r->d_pt[k], need));
-            r->pt_bytes[k] = need;
+            HIP_TRY(hipMalloc(&r->d_pt[k], slot_need));
+            r->pt_bytes[k] = slot_need;
         }
+        // this frame's results buffer was last read by the finish of two frames ago
+        if (pipe && !used[k] && r->pt_fin_set[par]) HIP_TRY(hipStreamWaitEvent(X, r->pt_fin[par], 0));
+        used[k] = true;
         char *b = static_cast<char *>(r->d_pt[k]);
         auto take = [&](size_t bytes) { char *q = b; b += (bytes + 255u) & ~(size_t)255u; return q; };
         PathArgs P{};
         P.state = reinterpret_cast<float4 *>(take(np * 32u));
-        P.result = reinterpret_cast<float4 *>(take(np * 16u));
         uint32_t *q0 = reinterpret_cast<uint32_t *>(take(qbytes));
         uint32_t *q1 = reinterpret_cast<uint32_t *>(take(qbytes));
         P.qcount = reinterpret_cast<uint32_t *>(take(cbytes));
@@ -696,6 +728,8 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         P.qhead = P.qcount + (size_t)(F.depth + 1) * kQueueSegs * 16u;
         P.dynamic = s->pt_dynamic ? 1 : 0;
         P.rec = reinterpret_cast<float4 *>(take((size_t)(F.depth - 1) * np * 32u));
+        // per-path radiance, indexed (sample - s0) * npix + pixel
+        P.result = pipe ? r->d_res[par] + (size_t)s0 * npix : reinterpret_cast<float4 *>(take(np * 16u));
         P.sum = r->d_sum;
         P.drain_level = drain_level;
         P.drain_below = 0;
@@ -718,21 +752,30 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
             if (level >= drain_level) break;           // that launch finished every remaining level
             if (level == 0) P.drain_below = (uint32_t)std::min<double>(4e9, s->pt_drain_rounds * resident);
         }
-        // the finishing pass: in sample order after the previous batch's (the running sum), and
-        // after the caller's earlier work (the accumulator and output)
-        if (pipe) {
-            HIP_TRY(hipStreamWaitEvent(X, r->pt_entry, 0));
-            if (r->pt_last >= 0 && r->pt_last != k) HIP_TRY(hipStreamWaitEvent(X, r->pt_fin[r->pt_last], 0));
-        }
-        const bool last = s0 + P.batch_spp >= F.spp;
-        if (s->ext) kext::launch_pt_finish(F, P, last, X);
-        else kcore::launch_pt_finish(F, P, last, X);
-        if (pipe) {
-            HIP_TRY(hipEventRecord(r->pt_fin[k], X));
-            r->pt_last = k;
+        if (!pipe) {   // serial: this batch's samples onto the running sum (the last: accumulate, RGB8)
+            const bool last = s0 + P.batch_spp >= F.spp;
+            if (s->ext) kext::launch_pt_finish(F, P, last, st);
+            else kcore::launch_pt_finish(F, P, last, st);
         }
     }
-    if (pipe) HIP_TRY(hipStreamWaitEvent(st, r->pt_fin[r->pt_last], 0));   // the frame, in the caller's order
+    if (pipe) {
+        // one finishing pass on the caller's stream: every sample of the frame in sample order
+        // (the same float sums as the batched running sum), after every batch's levels
+        for (int k = 0; k < 2; ++k)
+            if (used[k]) {
+                HIP_TRY(hipEventRecord(r->pt_lv[k], r->pt_stream[k]));
+                HIP_TRY(hipStreamWaitEvent(st, r->pt_lv[k], 0));
+            }
+        PathArgs P{};
+        P.result = r->d_res[par];
+        P.sum = r->d_sum;
+        P.s0 = 0;
+        P.batch_spp = F.spp;
+        if (s->ext) kext::launch_pt_finish(F, P, true, st);
+        else kcore::launch_pt_finish(F, P, true, st);
+        HIP_TRY(hipEventRecord(r->pt_fin[par], st));
+        r->pt_fin_set[par] = true;
+    }
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }
@@ -1279,10 +1322,11 @@ int rt_renderer_destroy(rt_renderer *r) {
     if (r->d_rgb) (void)hipFree(r->d_rgb);
     for (int k = 0; k < 2; ++k) {
         if (r->d_pt[k]) (void)hipFree(r->d_pt[k]);
+        if (r->d_res[k]) (void)hipFree(r->d_res[k]);
         if (r->pt_stream[k]) (void)hipStreamDestroy(r->pt_stream[k]);
+        if (r->pt_lv[k]) (void)hipEventDestroy(r->pt_lv[k]);
         if (r->pt_fin[k]) (void)hipEventDestroy(r->pt_fin[k]);
     }
-    if (r->pt_entry) (void)hipEventDestroy(r->pt_entry);
     if (r->d_sum) (void)hipFree(r->d_sum);
     if (r->d_samples) (void)hipFree(r->d_samples);
     if (r->d_order) (void)hipFree(r->d_order);

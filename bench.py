@@ -24,6 +24,12 @@ import os
 import sys
 import time
 
+# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process (4 by default); the
+# renderer's two path-tracing streams then share a queue with the launch stream, whose
+# finishing-pass barrier holds back the next frame's levels: 8 queues, CFG3-sub 2.05 -> 1.92 ms
+# (profiles/r02/bench_pipe_bhq*.json).  Set before HIP initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import numpy as np
 import torch
 

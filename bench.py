@@ -24,14 +24,32 @@ import os
 import sys
 import time
 
-# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process (4 by default); the
-# renderer's two path-tracing streams then share a queue with the launch stream, whose
-# finishing-pass barrier holds back the next frame's levels: 8 queues, CFG3-sub 2.05 -> 1.92 ms
-# (profiles/r02/bench_pipe_bhq*.json).  Set before HIP initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
-import numpy as np
-import torch
+def _path_traced(argv):
+    """Trace depth > 1 for this command line (--config / --depth), before anything loads HIP."""
+    cfg, depth = 2, None
+    for i, a in enumerate(argv):
+        key, _, val = a.partition("=")
+        if not val and i + 1 < len(argv):
+            val = argv[i + 1]
+        if key == "--config":
+            cfg = int(val)
+        elif key == "--depth":
+            depth = int(val)
+    return (depth if depth is not None else {3: 4, 5: 10}.get(cfg, 1)) > 1
+
+
+# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process (4 by default).  Path
+# tracing: the renderer's two path streams then share a queue with the launch stream, whose
+# finishing-pass barrier holds back the next frame's levels -- 8 queues, CFG3-sub 2.05 -> 1.92
+# ms (profiles/r02/bench_pipe_bhq*.json).  Primary+shadow multi-GPU frames go the other way
+# (their per-frame cross-stream waits cost more across queues: 0.119 -> 0.144 ms at world 1,
+# profiles/r02/multi_overhead_hwq.json), so they keep HIP's default.  Set before HIP initialises.
+if _path_traced(sys.argv[1:]):
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

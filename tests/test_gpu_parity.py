@@ -500,6 +500,34 @@ def test_pipelined_batches_equal_serial(rt, torch, monkeypatch, recipe, W, H, me
 
 
 @pytest.mark.gpu
+def test_pipelined_frames_switch_to_serial_and_back(rt, torch, monkeypatch):
+    """A frame whose per-sample results exceed the 2 GB result buffer (1080p at 65 spp) runs the
+    serial path on the caller's stream between pipelined frames, all submitted back to back:
+    frames and accumulator equal an all-serial renderer's."""
+    W, H = 1920, 1080
+    monkeypatch.setenv("RT_PT_PIPELINE", "0")
+    s0 = rt.Scene.recipe("teapotF")
+    monkeypatch.setenv("RT_PT_PIPELINE", "1")
+    s1 = rt.Scene.recipe("teapotF")
+    r0, r1 = rt.Renderer(s0, W, H), rt.Renderer(s1, W, H)
+    plan = [(2, 4), (65, 2), (2, 4), (1, 3)]
+    st = torch.cuda.Stream()
+    outs = []
+    with torch.cuda.stream(st):
+        for r in (r0, r1):
+            frames = []
+            for f, (spp, depth) in enumerate(plan):
+                o = torch.zeros(W * H, dtype=torch.int32, device="cuda:0")
+                r.Tick(o, spp=spp, depth=depth, frame=f, stream=st.cuda_stream)
+                frames.append(o)
+            outs.append(frames)
+    torch.cuda.synchronize()
+    for f in range(len(plan)):
+        assert torch.equal(outs[0][f], outs[1][f]), f"frame {f} differs"
+    assert np.array_equal(r0.accumulator(), r1.accumulator())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("recipe,W,H,spp,depth,mode,shards", [
     ("teapotF", 200, 120, 4, 1, 0, 1),      # primary+shadow, LDS kernel
     ("mig16", 160, 96, 3, 1, 0, 1),         # global-node kernel (wave walk AUTO)

@@ -681,8 +681,9 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         if (!r->pt_stream[0]) {
             for (int k = 0; k < 2; ++k) {
                 HIP_TRY(hipStreamCreateWithFlags(&r->pt_stream[k], hipStreamNonBlocking));
-                HIP_TRY(hipEventCreateWithFlags(&r->pt_lv[k], hipEventDisableTiming));
-                HIP_TRY(hipEventCreateWithFlags(&r->pt_fin[k], hipEventDisableTiming));
+                // ordering between streams of this device only: a device-scope release
+                HIP_TRY(hipEventCreateWithFlags(&r->pt_lv[k], hipEventDisableTiming | hipEventReleaseToDevice));
+                HIP_TRY(hipEventCreateWithFlags(&r->pt_fin[k], hipEventDisableTiming | hipEventReleaseToDevice));
             }
         }
         par = r->pt_parity;

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -171,6 +172,15 @@ int gather(rt_comm *c, int k, hipStream_t st) {
     return RT_OK;
 }
 
+// The per-frame ordering events order work between streams of ONE device (render -> gather ->
+// unshuffle): a device-scope release is enough and cheaper than the default system-scope one
+// (world-1 pipelined frame 0.1205 -> 0.1181 ms, profiles/r02/multi_overhead_events.json);
+// RT_EVENT_SCOPE=system restores the default.
+unsigned sync_event_flags() {
+    const char *e = std::getenv("RT_EVENT_SCOPE");
+    return hipEventDisableTiming | (e && std::strcmp(e, "system") == 0 ? 0u : (unsigned)hipEventReleaseToDevice);
+}
+
 int assemble(rt_comm *c, rt_renderer *r, int k, uint32_t *rgb8, hipStream_t st) {
     if (c->rank != 0) return RT_OK;
     if (!rgb8) return fail(RT_ERR_INVALID, "rt_render_frame_multi: rank 0 needs an output frame");
@@ -297,9 +307,9 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
     if (!c->comm_stream) {
         HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
         for (int j = 0; j < 2; ++j) {
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_render[j], hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_gather[j], hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_asm[j], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_render[j], sync_event_flags()));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_gather[j], sync_event_flags()));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_asm[j], sync_event_flags()));
         }
     }
     if (c->pending >= 0) {

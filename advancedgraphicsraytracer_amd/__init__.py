@@ -159,6 +159,7 @@ def lib():
         "rt_assemble_shards": ([vp, vp, u32, vp, vp], C.c_int),
         "rt_renderer_counters": ([vp, C.POINTER(Counters)], C.c_int),
         "rt_renderer_read_accumulator": ([vp, fp], C.c_int),
+        "rt_renderer_overlap": ([vp, C.POINTER(C.c_int), fp], C.c_int),
         "rt_renderer_stream": ([vp, C.POINTER(vp)], C.c_int),
         "rt_frame_kernel_name": ([vp, C.POINTER(FrameParams)], C.c_char_p),
         "rt_synchronize": ([vp], C.c_int),
@@ -659,6 +660,14 @@ class Renderer:
         c = Counters()
         _check(self.L.rt_renderer_counters(self.h, C.byref(c)))
         return {n: int(getattr(c, n)) for n, _ in Counters._fields_}
+
+    def overlap(self):
+        """Overlapped primary+shadow frames: (state, group ms) -- state 1 overlapped, 0 serial,
+        -1 not decided yet; ms = the timed groups (serial, overlapped, overlapped, serial)."""
+        st = C.c_int()
+        ms = np.zeros(4, np.float32)
+        _check(self.L.rt_renderer_overlap(self.h, C.byref(st), _fptr(ms)))
+        return st.value, [round(float(x), 4) for x in ms]
 
     def accumulator(self):
         acc = np.zeros((self.height * self.width, 4), np.float32)

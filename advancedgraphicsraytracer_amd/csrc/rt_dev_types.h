@@ -62,7 +62,8 @@ struct FrameArgs {
     uint32_t W, H, spp, depth, frame, reset;
     uint32_t shard, nshards, tiles_x, ntiles_local;
     uint32_t nchunks, nunits;           // sample chunks per tile (1 = no split); ntiles_local * nchunks
-    float4 *samples;                    // nchunks > 1: per-sample values [spp][ntiles_local][64]
+    float4 *samples;                    // non-null: per-sample values [spp][ntiles_local][64] (sample
+                                        // split, overlapped frames); k_pt_finish accumulates them
     int packed_out;
     const uint32_t *order;              // tile dispatch order: local tile of slot i (nullptr = identity)
     uint32_t *tile_cost;                // if set: each tile's wave cycles (to build the order)

@@ -73,6 +73,8 @@ struct rt_scene {
                                               // of the 288 GB HBM holds all 16 spp of a 1080p depth-10 frame
     bool pt_pipeline = true;        // sample batches alternate path-state slots and streams
                                     // (RT_PT_PIPELINE=0: one slot, the caller's stream)
+    int32_t ps_pipeline = -1;       // primary+shadow frames overlap: -1 timed per renderer (auto),
+                                    // 0 never, 1 always (RT_PS_PIPELINE)
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
     void *d_xprims = nullptr, *d_tex = nullptr, *d_pairs = nullptr, *d_pairs48 = nullptr, *d_words = nullptr;
     void *d_scratch = nullptr;  // staging for the host-pointer batched calls
@@ -122,6 +124,18 @@ struct rt_renderer {
     bool pt_fin_set[2] = {false, false};
     int pt_slot = 0, pt_parity = 0;
     bool pt_serial_last = false;    // the last path-traced frame ran the serial path
+    // overlapped primary+shadow frames (launch_render): with RT_PS_PIPELINE auto, four groups of
+    // kPsGroup eligible frames back to back -- serial, overlapped, overlapped, serial, so that the
+    // clock ramp of a fresh process cancels -- are timed on the caller's stream (events
+    // pev[2g], pev[2g + 1] around group g); the next frame keeps the faster mode for the
+    // parameter set
+    int ps_phase = 0;               // 0 .. 4 kPsGroup - 1 timing frames, 4 kPsGroup decide, -1 decided
+    bool ps_use = false;
+    uint64_t ps_last = 0;           // r->frames at the last timing frame (any other frame restarts)
+    bool ps_prev = false;           // the previous eligible frame ran overlapped
+    hipEvent_t pev[8] = {};
+    hipEvent_t ps_join = nullptr;   // caller's stream -> overlap stream, on a switch to overlapped
+    float ps_ms[4] = {};
     // per-sample values of sample-split frames (FrameArgs::samples)
     void *d_samples = nullptr;
     size_t samples_bytes = 0;
@@ -589,6 +603,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     s->xcd_order = (size_t)s->bvh.nodes_used * 32u + (size_t)n * 48u > (4u << 20);
     if (const char *e = std::getenv("RT_XCD_ORDER")) s->xcd_order = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_PIPELINE")) s->pt_pipeline = std::atoi(e) != 0;
+    if (const char *e = std::getenv("RT_PS_PIPELINE")) s->ps_pipeline = std::max(-1, std::min(1, std::atoi(e)));
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
@@ -640,6 +655,31 @@ uint64_t frame_pixels(const rt_renderer *r, const FrameArgs &F, uint32_t shard, 
 }
 
 
+// The renderer's two overlap streams and their ordering events (created once).
+int ensure_pipe_streams(rt_renderer *r) {
+    if (r->pt_stream[0]) return RT_OK;
+    for (int k = 0; k < 2; ++k) {
+        HIP_TRY(hipStreamCreateWithFlags(&r->pt_stream[k], hipStreamNonBlocking));
+        // ordering between streams of this device only: a device-scope release
+        HIP_TRY(hipEventCreateWithFlags(&r->pt_lv[k], hipEventDisableTiming | hipEventReleaseToDevice));
+        HIP_TRY(hipEventCreateWithFlags(&r->pt_fin[k], hipEventDisableTiming | hipEventReleaseToDevice));
+    }
+    return RT_OK;
+}
+
+// The frame-level per-sample result buffer of parity `par`, grown to `bytes`.
+int ensure_res(rt_renderer *r, int par, uint64_t bytes) {
+    if (bytes <= r->res_bytes[par]) return RT_OK;
+    HIP_TRY(hipDeviceSynchronize());   // every pending use of the old buffer
+    if (r->d_res[par]) HIP_TRY(hipFree(r->d_res[par]));
+    r->d_res[par] = nullptr;
+    r->res_bytes[par] = 0;
+    r->pt_fin_set[par] = false;
+    HIP_TRY(hipMalloc(&r->d_res[par], bytes));
+    r->res_bytes[par] = bytes;
+    return RT_OK;
+}
+
 // Wavefront path tracing of one frame / shard (PathArgs, rt_dev_types.h): the samples are
 // processed in batches that fit RT_PT_MEM_MB (default 12288 MB) of path state; per batch
 // one k_pt_level launch per bounce level, then k_pt_finish.
@@ -678,25 +718,11 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     if (pipe && r->pt_serial_last) HIP_TRY(hipStreamSynchronize(st));
     r->pt_serial_last = !pipe;
     if (pipe) {
-        if (!r->pt_stream[0]) {
-            for (int k = 0; k < 2; ++k) {
-                HIP_TRY(hipStreamCreateWithFlags(&r->pt_stream[k], hipStreamNonBlocking));
-                // ordering between streams of this device only: a device-scope release
-                HIP_TRY(hipEventCreateWithFlags(&r->pt_lv[k], hipEventDisableTiming | hipEventReleaseToDevice));
-                HIP_TRY(hipEventCreateWithFlags(&r->pt_fin[k], hipEventDisableTiming | hipEventReleaseToDevice));
-            }
-        }
+        int rc = ensure_pipe_streams(r);
+        if (rc != RT_OK) return rc;
         par = r->pt_parity;
         r->pt_parity ^= 1;
-        if (res_need > r->res_bytes[par]) {
-            HIP_TRY(hipDeviceSynchronize());   // every pending use of the old buffer
-            if (r->d_res[par]) HIP_TRY(hipFree(r->d_res[par]));
-            r->d_res[par] = nullptr;
-            r->res_bytes[par] = 0;
-            r->pt_fin_set[par] = false;
-            HIP_TRY(hipMalloc(&r->d_res[par], res_need));
-            r->res_bytes[par] = res_need;
-        }
+        if ((rc = ensure_res(r, par, res_need)) != RT_OK) return rc;
     }
     bool used[2] = {false, false};
     const size_t lds = stack_bytes(s);
@@ -867,6 +893,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
     if (key != r->order_key || n != r->order_n) {
         r->order_key = key;
         r->order_state = 0;
+        r->ps_phase = 0;   // the overlap decision belongs to the parameter set too
         if (n != r->order_n) {
             HIP_TRY(hipDeviceSynchronize());                             // frames may still read them
             if (r->d_order) HIP_TRY(hipFree(r->d_order));
@@ -944,6 +971,8 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
     }
     return RT_OK;
 }
+
+constexpr int kPsGroup = 8;   // frames per timed group of the overlap decision
 
 int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
                   uint32_t *out, int packed, void *stream) {
@@ -1064,6 +1093,70 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         if (rc != RT_OK) return rc;
         if (lds_kind == 0) L.grid = dim3((F.nunits + 3) / 4);
     }
+    // Overlapped primary+shadow frames: each pixel's accumulator update has to follow the
+    // previous frame's, but its traversal does not.  Once the frame is in its steady state
+    // (no timing events, no cost recording) the frame kernel runs on one of the renderer's
+    // two overlap streams (by frame parity) and stores its samples in the frame-level result
+    // buffer of that parity; a finishing pass on the caller's stream then does the running
+    // average + RGB8 (k_pt_finish, the same float operations as the kernel's own epilogue).
+    // Frame f+1's waves so fill the CUs that frame f's tail leaves idle.  The kernel touches
+    // only renderer-private memory; a stream waits only for the finishing pass that last read
+    // its result buffer (two frames back).
+    // It pays where a frame is latency- or tail-bound (mig29 x16 1080p 0.411 -> 0.343 ms, 720p
+    // 0.385 -> 0.255 ms) and costs where it is issue-bound (TEAPOT-F 1080p 0.103 -> 0.126 ms: the
+    // finishing pass's 100 MB and two cross-stream waits per frame are not hidden), and only
+    // when the caller submits frames back to back -- so by default each renderer times both
+    // modes on its own frames and keeps the faster (RT_PS_PIPELINE: -1 auto, 0 off, 1 on).
+    const uint64_t ps_res = (uint64_t)p->spp * F.ntiles_local * 64u * 16u;
+    const bool ps_ok = s->ps_pipeline != 0 && mode == RT_MODE_PATH && md == 1 && lds_kind == 0 && F.nchunks <= 1 &&
+                       timed < 0 && split_timed < 0 && !F.tile_cost && !walk_pending && ps_res <= (2ull << 30);
+    bool ps_pipe = ps_ok && s->ps_pipeline == 1;
+    int ps_ev0 = -1, ps_ev1 = -1;   // pev recorded on the caller's stream before / after this frame
+    if (ps_ok && s->ps_pipeline < 0) {
+        constexpr int G = kPsGroup;
+        if (r->ps_phase > 0 && r->ps_phase < 4 * G && r->frames != r->ps_last + 1) r->ps_phase = 0;   // interrupted
+        if (r->ps_phase == 4 * G) {
+            HIP_TRY(hipEventSynchronize(r->pev[7]));
+            for (int g = 0; g < 4; ++g) HIP_TRY(hipEventElapsedTime(&r->ps_ms[g], r->pev[2 * g], r->pev[2 * g + 1]));
+            r->ps_use = r->ps_ms[1] + r->ps_ms[2] < r->ps_ms[0] + r->ps_ms[3];
+            r->ps_phase = -1;
+        }
+        if (r->ps_phase >= 0) {
+            if (r->ps_phase == 0) {   // streams, events and both result buffers before the timing
+                if (!r->pev[0])
+                    for (auto &e : r->pev) HIP_TRY(hipEventCreate(&e));
+                int rc = ensure_pipe_streams(r);
+                for (int k = 0; k < 2 && rc == RT_OK; ++k) rc = ensure_res(r, k, ps_res);
+                if (rc != RT_OK) return rc;
+            }
+            const int g = r->ps_phase / G;   // serial, overlapped, overlapped, serial
+            ps_pipe = g == 1 || g == 2;
+            if (r->ps_phase % G == 0) ps_ev0 = 2 * g;
+            if (r->ps_phase % G == G - 1) ps_ev1 = 2 * g + 1;
+            r->ps_last = r->frames;
+            ++r->ps_phase;
+        } else {
+            ps_pipe = r->ps_use;
+        }
+    }
+    if (ps_ev0 >= 0) HIP_TRY(hipEventRecord(r->pev[ps_ev0], st));
+    int par = 0;
+    if (ps_pipe) {
+        int rc = ensure_pipe_streams(r);
+        if (rc != RT_OK) return rc;
+        par = r->pt_parity;
+        r->pt_parity ^= 1;
+        if ((rc = ensure_res(r, par, ps_res)) != RT_OK) return rc;
+        L.stream = r->pt_stream[par];
+        if (r->pt_fin_set[par]) HIP_TRY(hipStreamWaitEvent(L.stream, r->pt_fin[par], 0));
+        if (!r->ps_prev) {   // switching from serial frames: start behind the caller's stream
+            if (!r->ps_join) HIP_TRY(hipEventCreateWithFlags(&r->ps_join, hipEventDisableTiming | hipEventReleaseToDevice));
+            HIP_TRY(hipEventRecord(r->ps_join, st));
+            HIP_TRY(hipStreamWaitEvent(L.stream, r->ps_join, 0));
+        }
+        F.samples = r->d_res[par];
+    }
+    if (ps_ok) r->ps_prev = ps_pipe;
     if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed], st));
     if (split_timed >= 0) HIP_TRY(hipEventRecord(r->sev[2 * split_timed], st));
     if (s->ext) kext::launch_frame(view, F, L);
@@ -1071,14 +1164,23 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     HIP_TRY(hipGetLastError());
     if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed + 1], st));
     if (split_timed >= 0) HIP_TRY(hipEventRecord(r->sev[2 * split_timed + 1], st));
-    if (F.nchunks > 1) {   // the pixels' samples in sample order, running average, RGB8
+    if (ps_pipe) {
+        HIP_TRY(hipEventRecord(r->pt_lv[par], L.stream));
+        HIP_TRY(hipStreamWaitEvent(st, r->pt_lv[par], 0));
+    }
+    if (F.samples) {   // the pixels' samples in sample order, running average, RGB8
         PathArgs P{};
         P.batch_spp = p->spp;
         P.result = F.samples;
         if (s->ext) kext::launch_pt_finish(F, P, true, st);
         else kcore::launch_pt_finish(F, P, true, st);
         HIP_TRY(hipGetLastError());
+        if (ps_pipe) {
+            HIP_TRY(hipEventRecord(r->pt_fin[par], st));
+            r->pt_fin_set[par] = true;
+        }
     }
+    if (ps_ev1 >= 0) HIP_TRY(hipEventRecord(r->pev[ps_ev1], st));
     (void)tiles_y;
     r->primary += frame_pixels(r, F, shard, nshards, tiles_x, ntiles) * p->spp;
     r->frames += 1;
@@ -1336,6 +1438,9 @@ int rt_renderer_destroy(rt_renderer *r) {
         if (e) (void)hipEventDestroy(e);
     for (auto &e : r->sev)
         if (e) (void)hipEventDestroy(e);
+    for (auto &e : r->pev)
+        if (e) (void)hipEventDestroy(e);
+    if (r->ps_join) (void)hipEventDestroy(r->ps_join);
     (void)hipStreamDestroy(r->stream);
     delete r;
     return RT_OK;
@@ -1394,6 +1499,15 @@ int rt_renderer_counters(rt_renderer *r, rt_counters *out) {
         out->bounce += c[(size_t)k * 8 + 1];
     }
     out->frames = r->frames;
+    return RT_OK;
+}
+
+int rt_renderer_overlap(const rt_renderer *r, int *state, float ms[4]) {
+    if (!r || !state) return fail(RT_ERR_INVALID, "rt_renderer_overlap: null argument");
+    const int32_t mode = r->scene->ps_pipeline;
+    *state = mode >= 0 ? mode : (r->ps_phase == -1 ? (r->ps_use ? 1 : 0) : -1);
+    if (ms)
+        for (int g = 0; g < 4; ++g) ms[g] = (mode < 0 && r->ps_phase == -1) ? r->ps_ms[g] : 0.0f;
     return RT_OK;
 }
 

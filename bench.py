@@ -160,10 +160,10 @@ def cpu_baseline(args, spp):
     return out
 
 
-def companion_rate(scene, W, H, spp, depth, stream, device, warm=30, frames=300):
+def companion_rate(scene, W, H, spp, depth, stream, device, warm=60, frames=300):
     """The same workload at another frame size on a renderer of its own (BASELINE.json's
-    metric is quoted at 1280x720 and 1920x1080): warm-up frames (camera-walk and tile-order
-    tuning), then `frames` timed frames between two stream events and a wall clock."""
+    metric is quoted at 1280x720 and 1920x1080): warm-up frames (camera-walk, tile-order and
+    frame-overlap tuning), then `frames` timed frames between two stream events and a wall clock."""
     r = rt.Renderer(scene, W, H)
     out = torch.zeros(W * H, dtype=torch.int32, device=f"cuda:{device}")
     sptr = stream.cuda_stream
@@ -182,7 +182,7 @@ def companion_rate(scene, W, H, spp, depth, stream, device, warm=30, frames=300)
         wall = time.perf_counter() - t0
     c1 = r.counters()
     rays = sum(c1[k] - c0[k] for k in ("primary", "shadow", "bounce"))
-    return {"width": W, "height": H, "spp": spp, "depth": depth, "frames": frames,
+    return {"width": W, "height": H, "spp": spp, "depth": depth, "frames": frames, "overlapped": r.overlap()[0],
             "ms_per_frame": round(wall / frames * 1e3, 4), "frame_ms_events": round(e0.elapsed_time(e1) / frames, 4),
             "mrays_s": round(rays / wall / 1e6, 3), "fps": round(frames / wall, 3)}
 
@@ -322,6 +322,7 @@ def main():
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     tot_rays, tot_primary, tot_shadow, tot_bounce = local_rays.tolist()
     wall = t_max.item()
+    overlap = rend.overlap()
     companion = None
     if world == 1 and args.depth == 1 and (W, H) == (1920, 1080):   # the metric's other frame size
         companion = companion_rate(scene, 1280, 720, spp, args.depth, stream, device)
@@ -333,8 +334,10 @@ def main():
         roof = None
         default_workload = (args.scene, W, H, args.spp, args.depth) == (cfg["scene"], 1920, 1080, cfg["spp"], cfg["depth"])
         if key in summary and default_workload:
-            # one kernel per frame (depth 1, N = 1): its live duration is the frame's event time
-            live = frame_ms if (args.depth == 1 and world == 1) else None
+            # one kernel per frame (depth 1, N = 1, serial frames): its live duration is the
+            # frame's event time; overlapped frames share the CUs, so the kernel trace's duration
+            # of a serial run is used instead
+            live = frame_ms if (args.depth == 1 and world == 1 and overlap[0] != 1) else None
             bp, bs = BYTES_PER_RAY.get(args.scene, (None, None))
             alg = (primary * bp + shadow * bs) / args.steps if (bp and live) else None
             roof = rl.roofline(summary[key], kernel_ms=live, algorithmic_bytes=alg)
@@ -369,6 +372,9 @@ def main():
             "frame_ms_events": round(frame_ms, 4),
             "roofline": roof,
         }
+        if args.depth == 1:   # RT_PS_PIPELINE: serial or overlapped primary+shadow frames (rank 0)
+            line["overlapped_frames"] = {"state": overlap[0], "timed_groups_ms": overlap[1],
+                                         "groups": "serial, overlapped, overlapped, serial (8 frames each)"}
         if multi:
             line["multi_gpu"] = multi
         if companion:

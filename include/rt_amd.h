@@ -277,6 +277,13 @@ int rt_multi_flush(rt_renderer *r, rt_comm *c, uint32_t *rgb8_dev, void *stream)
 int rt_comm_timing(rt_comm *c, double *render_ms, double *gather_ms, uint64_t *frames);
 
 int rt_renderer_counters(rt_renderer *r, rt_counters *out);
+/* Overlapped primary+shadow frames (RT_PS_PIPELINE; no reference counterpart -- Renderer::Tick,
+ * renderer.cpp:200-309, is one serial pass): *state = 1 this renderer's primary+shadow frames
+ * run overlapped (frame kernel on a renderer stream, accumulate + RGB8 in a finishing pass on
+ * the caller's stream), 0 serial, -1 not decided yet (RT_PS_PIPELINE=-1 times both modes on
+ * the first eligible frames); ms (may be NULL) = the four timed groups' milliseconds (serial,
+ * overlapped, overlapped, serial) when decided by timing, else zeros. */
+int rt_renderer_overlap(const rt_renderer *r, int *state, float ms[4]);
 /* accumulator readback, W*H float4 */
 int rt_renderer_read_accumulator(rt_renderer *r, float *host_out);
 /* Name of the frame kernel rt_render_frame / rt_render_shard launch for these params

@@ -73,6 +73,7 @@ struct rt_scene {
                                               // of the 288 GB HBM holds all 16 spp of a 1080p depth-10 frame
     bool pt_pipeline = true;        // sample batches alternate path-state slots and streams
                                     // (RT_PT_PIPELINE=0: one slot, the caller's stream)
+    uint32_t ps_buffers = 3;        // per-sample result buffers of overlapped frames (RT_PS_BUFFERS, 2-4)
     int32_t ps_pipeline = -1;       // primary+shadow frames overlap: -1 timed per renderer (auto),
                                     // 0 never, 1 always (RT_PS_PIPELINE)
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
@@ -136,6 +137,14 @@ struct rt_renderer {
     hipEvent_t pev[8] = {};
     hipEvent_t ps_join = nullptr;   // caller's stream -> overlap stream, on a switch to overlapped
     float ps_ms[4] = {};
+    // the overlapped frames' per-sample results, frame n in buffer n % ps_buffers (kernel on
+    // renderer stream n % 2): frame n + ps_buffers waits for the finishing pass of frame n only,
+    // so a kernel never waits for the finish of the frame just before the one running beside it
+    float4 *ps_res[4] = {};
+    size_t ps_res_bytes[4] = {};
+    hipEvent_t ps_fin[4] = {};
+    bool ps_fin_set[4] = {};
+    uint32_t ps_count = 0;
     // per-sample values of sample-split frames (FrameArgs::samples)
     void *d_samples = nullptr;
     size_t samples_bytes = 0;
@@ -604,6 +613,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_XCD_ORDER")) s->xcd_order = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_PIPELINE")) s->pt_pipeline = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PS_PIPELINE")) s->ps_pipeline = std::max(-1, std::min(1, std::atoi(e)));
+    if (const char *e = std::getenv("RT_PS_BUFFERS")) s->ps_buffers = (uint32_t)std::max(2, std::min(4, std::atoi(e)));
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
@@ -677,6 +687,20 @@ int ensure_res(rt_renderer *r, int par, uint64_t bytes) {
     r->pt_fin_set[par] = false;
     HIP_TRY(hipMalloc(&r->d_res[par], bytes));
     r->res_bytes[par] = bytes;
+    return RT_OK;
+}
+
+// Overlapped primary+shadow frames' result buffer b, grown to `bytes` (launch_render).
+int ensure_ps_res(rt_renderer *r, uint32_t b, uint64_t bytes) {
+    if (!r->ps_fin[b]) HIP_TRY(hipEventCreateWithFlags(&r->ps_fin[b], hipEventDisableTiming | hipEventReleaseToDevice));
+    if (bytes <= r->ps_res_bytes[b]) return RT_OK;
+    HIP_TRY(hipDeviceSynchronize());   // every pending use of the old buffer
+    if (r->ps_res[b]) HIP_TRY(hipFree(r->ps_res[b]));
+    r->ps_res[b] = nullptr;
+    r->ps_res_bytes[b] = 0;
+    r->ps_fin_set[b] = false;
+    HIP_TRY(hipMalloc(&r->ps_res[b], bytes));
+    r->ps_res_bytes[b] = bytes;
     return RT_OK;
 }
 
@@ -1102,14 +1126,18 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     // Frame f+1's waves so fill the CUs that frame f's tail leaves idle.  The kernel touches
     // only renderer-private memory; a stream waits only for the finishing pass that last read
     // its result buffer (two frames back).
-    // It pays where a frame is latency- or tail-bound (mig29 x16 1080p 0.411 -> 0.343 ms, 720p
-    // 0.385 -> 0.255 ms) and costs where it is issue-bound (TEAPOT-F 1080p 0.103 -> 0.126 ms: the
-    // finishing pass's 100 MB and two cross-stream waits per frame are not hidden), and only
+    // Three result buffers (RT_PS_BUFFERS): with two, frame f + 2's kernel waited for frame f's
+    // finishing pass while frame f + 1's kernel shared the CUs, which put the finishing pass and
+    // two cross-stream waits on the critical path (TEAPOT-F 1080p 0.119 ms per frame vs 0.1055
+    // with three; four measure the same as three; profiles/r02/ps_window*.log).
+    // It pays where a frame is latency- or tail-bound (mig29 x16 1080p 0.41 -> 0.33 ms, 720p
+    // 0.385 -> 0.255 ms) and costs where it is issue-bound (TEAPOT-F 1080p 0.1024 -> 0.1055 ms:
+    // the finishing pass's extra 66 MB of sample traffic is not hidden there), and only
     // when the caller submits frames back to back -- so by default each renderer times both
     // modes on its own frames and keeps the faster (RT_PS_PIPELINE: -1 auto, 0 off, 1 on).
-    const uint64_t ps_res = (uint64_t)p->spp * F.ntiles_local * 64u * 16u;
+    const uint64_t ps_bytes = (uint64_t)p->spp * F.ntiles_local * 64u * 16u;
     const bool ps_ok = s->ps_pipeline != 0 && mode == RT_MODE_PATH && md == 1 && lds_kind == 0 && F.nchunks <= 1 &&
-                       timed < 0 && split_timed < 0 && !F.tile_cost && !walk_pending && ps_res <= (2ull << 30);
+                       timed < 0 && split_timed < 0 && !F.tile_cost && !walk_pending && ps_bytes <= (2ull << 30);
     bool ps_pipe = ps_ok && s->ps_pipeline == 1;
     int ps_ev0 = -1, ps_ev1 = -1;   // pev recorded on the caller's stream before / after this frame
     if (ps_ok && s->ps_pipeline < 0) {
@@ -1126,7 +1154,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
                 if (!r->pev[0])
                     for (auto &e : r->pev) HIP_TRY(hipEventCreate(&e));
                 int rc = ensure_pipe_streams(r);
-                for (int k = 0; k < 2 && rc == RT_OK; ++k) rc = ensure_res(r, k, ps_res);
+                for (uint32_t k = 0; k < s->ps_buffers && rc == RT_OK; ++k) rc = ensure_ps_res(r, k, ps_bytes);
                 if (rc != RT_OK) return rc;
             }
             const int g = r->ps_phase / G;   // serial, overlapped, overlapped, serial
@@ -1140,21 +1168,23 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         }
     }
     if (ps_ev0 >= 0) HIP_TRY(hipEventRecord(r->pev[ps_ev0], st));
-    int par = 0;
+    uint32_t buf = 0;
+    int lane_st = 0;
     if (ps_pipe) {
         int rc = ensure_pipe_streams(r);
         if (rc != RT_OK) return rc;
-        par = r->pt_parity;
-        r->pt_parity ^= 1;
-        if ((rc = ensure_res(r, par, ps_res)) != RT_OK) return rc;
-        L.stream = r->pt_stream[par];
-        if (r->pt_fin_set[par]) HIP_TRY(hipStreamWaitEvent(L.stream, r->pt_fin[par], 0));
+        buf = r->ps_count % s->ps_buffers;
+        lane_st = (int)(r->ps_count & 1u);
+        ++r->ps_count;
+        if ((rc = ensure_ps_res(r, buf, ps_bytes)) != RT_OK) return rc;
+        L.stream = r->pt_stream[lane_st];
+        if (r->ps_fin_set[buf]) HIP_TRY(hipStreamWaitEvent(L.stream, r->ps_fin[buf], 0));
         if (!r->ps_prev) {   // switching from serial frames: start behind the caller's stream
             if (!r->ps_join) HIP_TRY(hipEventCreateWithFlags(&r->ps_join, hipEventDisableTiming | hipEventReleaseToDevice));
             HIP_TRY(hipEventRecord(r->ps_join, st));
             HIP_TRY(hipStreamWaitEvent(L.stream, r->ps_join, 0));
         }
-        F.samples = r->d_res[par];
+        F.samples = r->ps_res[buf];
     }
     if (ps_ok) r->ps_prev = ps_pipe;
     if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed], st));
@@ -1165,8 +1195,8 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed + 1], st));
     if (split_timed >= 0) HIP_TRY(hipEventRecord(r->sev[2 * split_timed + 1], st));
     if (ps_pipe) {
-        HIP_TRY(hipEventRecord(r->pt_lv[par], L.stream));
-        HIP_TRY(hipStreamWaitEvent(st, r->pt_lv[par], 0));
+        HIP_TRY(hipEventRecord(r->pt_lv[lane_st], L.stream));
+        HIP_TRY(hipStreamWaitEvent(st, r->pt_lv[lane_st], 0));
     }
     if (F.samples) {   // the pixels' samples in sample order, running average, RGB8
         PathArgs P{};
@@ -1176,8 +1206,8 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         else kcore::launch_pt_finish(F, P, true, st);
         HIP_TRY(hipGetLastError());
         if (ps_pipe) {
-            HIP_TRY(hipEventRecord(r->pt_fin[par], st));
-            r->pt_fin_set[par] = true;
+            HIP_TRY(hipEventRecord(r->ps_fin[buf], st));
+            r->ps_fin_set[buf] = true;
         }
     }
     if (ps_ev1 >= 0) HIP_TRY(hipEventRecord(r->pev[ps_ev1], st));
@@ -1441,6 +1471,10 @@ int rt_renderer_destroy(rt_renderer *r) {
     for (auto &e : r->pev)
         if (e) (void)hipEventDestroy(e);
     if (r->ps_join) (void)hipEventDestroy(r->ps_join);
+    for (int b = 0; b < 4; ++b) {
+        if (r->ps_res[b]) (void)hipFree(r->ps_res[b]);
+        if (r->ps_fin[b]) (void)hipEventDestroy(r->ps_fin[b]);
+    }
     (void)hipStreamDestroy(r->stream);
     delete r;
     return RT_OK;

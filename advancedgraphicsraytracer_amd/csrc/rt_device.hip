@@ -116,13 +116,15 @@ struct rt_renderer {
     // caller's stream alone when pipelining is off or the results do not fit.
     void *d_pt[2] = {nullptr, nullptr};
     size_t pt_bytes[2] = {0, 0};
-    float4 *d_res[2] = {nullptr, nullptr};   // [sample][pixel] radiance of a frame, by frame parity
-    size_t res_bytes[2] = {0, 0};
+    // [sample][pixel] radiance of a frame, frame n in buffer n % kPtResBuffers: frame n + 3's
+    // batches wait for frame n's finishing pass only (see kPtResBuffers)
+    float4 *d_res[3] = {nullptr, nullptr, nullptr};
+    size_t res_bytes[3] = {0, 0, 0};
     float4 *d_sum = nullptr;        // the running sample sum across batches (serial path)
     hipStream_t pt_stream[2] = {nullptr, nullptr};
     hipEvent_t pt_lv[2] = {nullptr, nullptr};    // a path stream's levels of this frame are done
-    hipEvent_t pt_fin[2] = {nullptr, nullptr};   // the finish that read d_res[parity] is done
-    bool pt_fin_set[2] = {false, false};
+    hipEvent_t pt_fin[3] = {nullptr, nullptr, nullptr};   // the finish that read d_res[b] is done
+    bool pt_fin_set[3] = {false, false, false};
     int pt_slot = 0, pt_parity = 0;
     bool pt_serial_last = false;    // the last path-traced frame ran the serial path
     // overlapped primary+shadow frames (launch_render): with RT_PS_PIPELINE auto, four groups of
@@ -665,6 +667,14 @@ uint64_t frame_pixels(const rt_renderer *r, const FrameArgs &F, uint32_t shard, 
 }
 
 
+// Per-sample result buffers of pipelined path-traced frames: with two (by frame parity), frame
+// n + 2's batches waited for frame n's finishing pass, which itself follows frame n + 1's levels
+// on the caller's stream; three let a frame start behind the finish of the frame before last.
+#ifndef RT_PT_RES_BUFFERS
+#define RT_PT_RES_BUFFERS 3
+#endif
+constexpr int kPtResBuffers = RT_PT_RES_BUFFERS;   // 2 or 3
+
 // The renderer's two overlap streams and their ordering events (created once).
 int ensure_pipe_streams(rt_renderer *r) {
     if (r->pt_stream[0]) return RT_OK;
@@ -672,6 +682,8 @@ int ensure_pipe_streams(rt_renderer *r) {
         HIP_TRY(hipStreamCreateWithFlags(&r->pt_stream[k], hipStreamNonBlocking));
         // ordering between streams of this device only: a device-scope release
         HIP_TRY(hipEventCreateWithFlags(&r->pt_lv[k], hipEventDisableTiming | hipEventReleaseToDevice));
+    }
+    for (int k = 0; k < kPtResBuffers; ++k) {
         HIP_TRY(hipEventCreateWithFlags(&r->pt_fin[k], hipEventDisableTiming | hipEventReleaseToDevice));
     }
     return RT_OK;
@@ -745,7 +757,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         int rc = ensure_pipe_streams(r);
         if (rc != RT_OK) return rc;
         par = r->pt_parity;
-        r->pt_parity ^= 1;
+        r->pt_parity = (par + 1) % kPtResBuffers;
         if ((rc = ensure_res(r, par, res_need)) != RT_OK) return rc;
     }
     bool used[2] = {false, false};
@@ -1455,9 +1467,11 @@ int rt_renderer_destroy(rt_renderer *r) {
     if (r->d_rgb) (void)hipFree(r->d_rgb);
     for (int k = 0; k < 2; ++k) {
         if (r->d_pt[k]) (void)hipFree(r->d_pt[k]);
-        if (r->d_res[k]) (void)hipFree(r->d_res[k]);
         if (r->pt_stream[k]) (void)hipStreamDestroy(r->pt_stream[k]);
         if (r->pt_lv[k]) (void)hipEventDestroy(r->pt_lv[k]);
+    }
+    for (int k = 0; k < kPtResBuffers; ++k) {
+        if (r->d_res[k]) (void)hipFree(r->d_res[k]);
         if (r->pt_fin[k]) (void)hipEventDestroy(r->pt_fin[k]);
     }
     if (r->d_sum) (void)hipFree(r->d_sum);

@@ -1148,7 +1148,9 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     // when the caller submits frames back to back -- so by default each renderer times both
     // modes on its own frames and keeps the faster (RT_PS_PIPELINE: -1 auto, 0 off, 1 on).
     const uint64_t ps_bytes = (uint64_t)p->spp * F.ntiles_local * 64u * 16u;
-    const bool ps_ok = s->ps_pipeline != 0 && mode == RT_MODE_PATH && md == 1 && lds_kind == 0 && F.nchunks <= 1 &&
+    // (sample-split frames -- a multi-GPU rank's shard at spp N -- store their samples anyway;
+    // overlapped, they go to the result buffers instead of d_samples)
+    const bool ps_ok = s->ps_pipeline != 0 && mode == RT_MODE_PATH && md == 1 && lds_kind == 0 &&
                        timed < 0 && split_timed < 0 && !F.tile_cost && !walk_pending && ps_bytes <= (2ull << 30);
     bool ps_pipe = ps_ok && s->ps_pipeline == 1;
     int ps_ev0 = -1, ps_ev1 = -1;   // pev recorded on the caller's stream before / after this frame

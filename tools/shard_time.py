@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--frames", type=int, default=30)
     ap.add_argument("--w", type=int, default=1920)
     ap.add_argument("--h", type=int, default=1080)
+    ap.add_argument("--warm", type=int, default=8, help="untimed frames per renderer (tuning)")
+    ap.add_argument("--strong", action="store_true", help="spp 1 per shard (one frame split N ways)")
     a = ap.parse_args()
     scene = rt.Scene.recipe(a.scene)
     out = {}
@@ -37,30 +39,32 @@ def main():
             torch.cuda.synchronize()
     torch.cuda.synchronize()
     r0.close()
-    for n in (1, 2, 4, 8):   # 8 warm-up frames: walk timing + tile-order recording settle first
+    for n in (1, 2, 4, 8):   # warm-up frames: walk timing, tile order, frame-overlap timing settle first
         r = rt.Renderer(scene, a.w, a.h)
         cap = r.shard_capacity(n)
         tiles = torch.zeros(cap, dtype=torch.int32, device="cuda")
         st = torch.cuda.Stream()
-        for f in range(8):
-            r.render_shard(tiles, n - 1, n, spp=n, depth=a.depth, frame=f, stream=st.cuda_stream)
+        spp = 1 if a.strong else n
+        for f in range(a.warm):
+            r.render_shard(tiles, n - 1, n, spp=spp, depth=a.depth, frame=f, stream=st.cuda_stream)
         torch.cuda.synchronize()
         c0 = r.counters()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         with torch.cuda.stream(st):
             ev[0].record()
             for f in range(a.frames):
-                r.render_shard(tiles, n - 1, n, spp=n, depth=a.depth, frame=8 + f, stream=st.cuda_stream)
+                r.render_shard(tiles, n - 1, n, spp=spp, depth=a.depth, frame=a.warm + f, stream=st.cuda_stream)
             ev[1].record()
         torch.cuda.synchronize()
         c1 = r.counters()
         ms = ev[0].elapsed_time(ev[1]) / a.frames
         rays = sum(c1[k] - c0[k] for k in ("primary", "shadow", "bounce")) / a.frames
-        out[n] = {"ms_per_frame": round(ms, 4), "mrays_s_per_gpu": round(rays / (ms * 1e-3) / 1e6, 1)}
+        out[n] = {"ms_per_frame": round(ms, 4), "mrays_s_per_gpu": round(rays / (ms * 1e-3) / 1e6, 1),
+                  "overlapped": r.overlap()[0]}
         print(n, json.dumps(out[n]), flush=True)
         r.close()
     base = out[1]["mrays_s_per_gpu"]
-    print(json.dumps({"scene": a.scene, "depth": a.depth, "per_rank": out,
+    print(json.dumps({"scene": a.scene, "depth": a.depth, "strong": a.strong, "ps": os.environ.get("RT_PS_PIPELINE", "-1"), "per_rank": out,
                       "predicted_efficiency_without_gather": {n: round(v["mrays_s_per_gpu"] / base, 3) for n, v in out.items()}}))
 
 

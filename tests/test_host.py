@@ -237,3 +237,14 @@ def test_prebuilt_bvh_above_24bit_node_index_is_refused(rt):
     rc = rt.lib().rt_scene_create(C.byref(d), C.byref(h))
     assert rc == rt.RT_ERR_UNSUPPORTED, rt.lib().rt_last_error()
     assert b"2^24" in rt.lib().rt_last_error()
+
+
+def test_renderer_overlap_query_rejects_null_arguments(rt):
+    """rt_renderer_overlap (overlapped primary+shadow frames' state) checks its arguments on
+    the host before touching the renderer: no GPU needed."""
+    import ctypes as C
+    L = rt.lib()
+    st = C.c_int(7)
+    assert L.rt_renderer_overlap(None, C.byref(st), None) == rt.RT_ERR_INVALID
+    assert st.value == 7
+    assert b"rt_renderer_overlap" in L.rt_last_error()

@@ -42,10 +42,12 @@ def _path_traced(argv):
 # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process (4 by default).  Path
 # tracing: the renderer's two path streams then share a queue with the launch stream, whose
 # finishing-pass barrier holds back the next frame's levels -- 8 queues, CFG3-sub 2.05 -> 1.92
-# ms (profiles/r02/bench_pipe_bhq*.json).  Primary+shadow multi-GPU frames go the other way
-# (their per-frame cross-stream waits cost more across queues: 0.119 -> 0.144 ms at world 1,
-# profiles/r02/multi_overhead_hwq.json), so they keep HIP's default.  Set before HIP initialises.
-if _path_traced(sys.argv[1:]):
+# ms (profiles/r02/bench_pipe_bhq*.json).  Multi-GPU frames (N > 1) too, since overlapped
+# primary+shadow frames: their two renderer streams and the communicator's stream then no longer
+# share a queue with the caller's (world-1 multi frame, mig29 x16: 0.471 -> 0.327 ms; TEAPOT-F
+# 0.128 either way; profiles/r02/multi_overhead_hwq8.log).  Single-GPU primary+shadow runs keep
+# HIP's default.  Set before HIP initialises.
+if _path_traced(sys.argv[1:]) or int(os.environ.get("WORLD_SIZE", "1")) > 1:
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import numpy as np  # noqa: E402

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <fstream>
 #include <iterator>
+#include <limits>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -142,7 +143,73 @@ struct Reader {
             for (int k = 0; k < 6; ++k) f.push_back(ids[sel[k]]);
             return;
         }
-        for (size_t k = 1; k + 1 < n; ++k) { f.push_back(ids[0]); f.push_back(ids[k]); f.push_back(ids[k + 1]); }
+        ear_clip(ids);
+    }
+
+    // pnpoly, template/tiny_obj_loader.h:1407-1419 (float)
+    static bool inside3(const float *vx, const float *vy, float tx, float ty) {
+        bool c = false;
+        for (int i = 0, j = 2; i < 3; j = i++)
+            if (((vy[i] > ty) != (vy[j] > ty)) && (tx < (vx[j] - vx[i]) * (ty - vy[i]) / (vy[j] - vy[i]) + vx[i])) c = !c;
+        return c;
+    }
+
+    // Polygons of 5+ corners: tinyobj's built-in ear clipping (tiny_obj_loader.h:1705-1928,
+    // TINYOBJLOADER_USE_MAPBOX_EARCUT undefined, real_t = float): project on the two axes
+    // picked from the first corner with a non-zero cross product, then cut ears starting at
+    // guess_vert, skipping reflex corners and triangles that contain another corner.
+    void ear_clip(const std::vector<int> &ids) {
+        const size_t nv = v.size();
+        size_t npolys = ids.size();
+        size_t axes[2] = {1, 2};
+        for (size_t k = 0; k < npolys; ++k) {
+            const size_t a = (size_t)ids[k % npolys], b = (size_t)ids[(k + 1) % npolys], c = (size_t)ids[(k + 2) % npolys];
+            if (3 * a + 2 >= nv || 3 * b + 2 >= nv || 3 * c + 2 >= nv) continue;
+            const float e0x = v[3 * b] - v[3 * a], e0y = v[3 * b + 1] - v[3 * a + 1], e0z = v[3 * b + 2] - v[3 * a + 2];
+            const float e1x = v[3 * c] - v[3 * b], e1y = v[3 * c + 1] - v[3 * b + 1], e1z = v[3 * c + 2] - v[3 * b + 2];
+            const float cx = std::fabs(e0y * e1z - e0z * e1y);
+            const float cy = std::fabs(e0z * e1x - e0x * e1z);
+            const float cz = std::fabs(e0x * e1y - e0y * e1x);
+            const float eps = std::numeric_limits<float>::epsilon();
+            if (cx > eps || cy > eps || cz > eps) {
+                if (!(cx > cy && cx > cz)) {
+                    axes[0] = 0;
+                    if (cz > cx && cz > cy) axes[1] = 1;
+                }
+                break;
+            }
+        }
+        std::vector<int> rem(ids);
+        size_t guess = 0, iters = rem.size(), prev = rem.size();
+        auto coord = [&](int id, size_t ax) { return (size_t)id * 3 + ax < nv ? v[(size_t)id * 3 + ax] : 0.0f; };
+        while (rem.size() > 3 && iters > 0) {
+            npolys = rem.size();
+            if (guess >= npolys) guess -= npolys;
+            if (prev != npolys) { prev = npolys; iters = npolys; }
+            else --iters;
+            int ind[3];
+            float vx[3], vy[3];
+            for (size_t k = 0; k < 3; ++k) {
+                ind[k] = rem[(guess + k) % npolys];
+                const bool ok = (size_t)ind[k] * 3 + axes[0] < nv && (size_t)ind[k] * 3 + axes[1] < nv;
+                vx[k] = ok ? v[(size_t)ind[k] * 3 + axes[0]] : 0.0f;
+                vy[k] = ok ? v[(size_t)ind[k] * 3 + axes[1]] : 0.0f;
+            }
+            const float e0x = vx[1] - vx[0], e0y = vy[1] - vy[0], e1x = vx[2] - vx[1], e1y = vy[2] - vy[1];
+            const float cross = e0x * e1y - e0y * e1x;
+            const float area = (vx[0] * vy[1] - vy[0] * vx[1]) * 0.5f;
+            if (cross * area < 0.0f) { guess += 1; continue; }   // reflex corner
+            bool overlap = false;
+            for (size_t o = 3; o < npolys && !overlap; ++o) {
+                const int id = rem[(guess + o) % npolys];
+                if ((size_t)id * 3 + axes[0] >= nv || (size_t)id * 3 + axes[1] >= nv) continue;
+                overlap = inside3(vx, vy, coord(id, axes[0]), coord(id, axes[1]));
+            }
+            if (overlap) { guess += 1; continue; }
+            f.insert(f.end(), ind, ind + 3);                  // the ear
+            rem.erase(rem.begin() + (long)((guess + 1) % npolys));
+        }
+        if (rem.size() == 3) f.insert(f.end(), rem.begin(), rem.end());
     }
 
     int line(const std::string &ln) {

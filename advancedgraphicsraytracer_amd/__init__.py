@@ -34,7 +34,7 @@ WALK_LANE, WALK_WAVE, WALK_AUTO = 0, 1, 2
 BVH_PLAIN, BVH_SBVH = 0, 1
 # renderer.h:9, renderer.h:13, renderer.cpp:105 (TracePacket's bounces: Trace's default depth)
 DEFAULT_DEPTH = {MODE_PATH: 10, MODE_WHITTED: 20, MODE_PACKET: 10}
-RECIPES = ("teapotF", "teapot", "mig16", "cfg3", "cfg5")
+RECIPES = ("teapotF", "teapot", "mig16", "cfg3", "cfg5", "default")
 
 
 class RTError(RuntimeError):
@@ -160,6 +160,8 @@ def lib():
         "rt_renderer_counters": ([vp, C.POINTER(Counters)], C.c_int),
         "rt_renderer_read_accumulator": ([vp, fp], C.c_int),
         "rt_renderer_overlap": ([vp, C.POINTER(C.c_int), fp], C.c_int),
+        "rt_renderer_overlap_depth": ([vp, C.POINTER(C.c_int), fp], C.c_int),
+        "rt_renderer_tile_costs": ([vp, C.POINTER(u32), u32, C.POINTER(u32)], C.c_int),
         "rt_renderer_stream": ([vp, C.POINTER(vp)], C.c_int),
         "rt_frame_kernel_name": ([vp, C.POINTER(FrameParams)], C.c_char_p),
         "rt_synchronize": ([vp], C.c_int),
@@ -668,6 +670,23 @@ class Renderer:
         ms = np.zeros(4, np.float32)
         _check(self.L.rt_renderer_overlap(self.h, C.byref(st), _fptr(ms)))
         return st.value, [round(float(x), 4) for x in ms]
+
+    def overlap_depth(self):
+        """Primary+shadow frames in flight: (depth, group ms) -- 1 serial, 2..4 overlapped, -1 not
+        decided yet; ms = the six timed groups (serial, 2, 4, 4, 2, serial in flight)."""
+        d = C.c_int()
+        ms = np.zeros(6, np.float32)
+        _check(self.L.rt_renderer_overlap_depth(self.h, C.byref(d), _fptr(ms)))
+        return d.value, [round(float(x), 4) for x in ms]
+
+    def tile_costs(self):
+        """Per-local-tile wave cycles behind the measured tile order (empty until recorded)."""
+        n = C.c_uint32()
+        _check(self.L.rt_renderer_tile_costs(self.h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, np.uint32)
+        if n.value:
+            _check(self.L.rt_renderer_tile_costs(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), n.value, C.byref(n)))
+        return out
 
     def accumulator(self):
         acc = np.zeros((self.height * self.width, 4), np.float32)

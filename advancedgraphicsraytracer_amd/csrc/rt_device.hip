@@ -73,9 +73,11 @@ struct rt_scene {
                                               // of the 288 GB HBM holds all 16 spp of a 1080p depth-10 frame
     bool pt_pipeline = true;        // sample batches alternate path-state slots and streams
                                     // (RT_PT_PIPELINE=0: one slot, the caller's stream)
-    uint32_t ps_buffers = 3;        // per-sample result buffers of overlapped frames (RT_PS_BUFFERS, 2-4)
+    uint32_t ps_buffers = 0;        // per-sample result buffers of overlapped frames (RT_PS_BUFFERS,
+                                    // 2-5; 0 = frames in flight + 1)
     int32_t ps_pipeline = -1;       // primary+shadow frames overlap: -1 timed per renderer (auto),
                                     // 0 never, 1 always (RT_PS_PIPELINE)
+    uint32_t ps_depth = 2;          // frames in flight when forced (RT_PS_DEPTH, 2-4)
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
     void *d_xprims = nullptr, *d_tex = nullptr, *d_pairs = nullptr, *d_pairs48 = nullptr, *d_words = nullptr;
     void *d_scratch = nullptr;  // staging for the host-pointer batched calls
@@ -96,6 +98,7 @@ struct rt_renderer {
     // measured-cost tile order (tile_order_step): per-tile cycles of one frame (two cost
     // maps while the camera walk is being timed), longest tile first afterwards
     uint32_t *d_order = nullptr, *d_cost = nullptr;
+    std::vector<uint32_t> host_cost;   // the cost map the active order was sorted from (local tiles)
     uint32_t order_n = 0;
     uint64_t order_key = 0;
     int order_state = 0;        // 0 idle, 1 costs recorded, 2 order active
@@ -121,31 +124,33 @@ struct rt_renderer {
     float4 *d_res[3] = {nullptr, nullptr, nullptr};
     size_t res_bytes[3] = {0, 0, 0};
     float4 *d_sum = nullptr;        // the running sample sum across batches (serial path)
-    hipStream_t pt_stream[2] = {nullptr, nullptr};
-    hipEvent_t pt_lv[2] = {nullptr, nullptr};    // a path stream's levels of this frame are done
+    // renderer streams: the path tracer's two path streams are 0 and 1; overlapped primary+
+    // shadow frames use the first `depth` of them (frames in flight)
+    hipStream_t pt_stream[4] = {};
+    hipEvent_t pt_lv[4] = {};       // a renderer stream's work of this frame is done
     hipEvent_t pt_fin[3] = {nullptr, nullptr, nullptr};   // the finish that read d_res[b] is done
     bool pt_fin_set[3] = {false, false, false};
     int pt_slot = 0, pt_parity = 0;
     bool pt_serial_last = false;    // the last path-traced frame ran the serial path
-    // overlapped primary+shadow frames (launch_render): with RT_PS_PIPELINE auto, four groups of
-    // kPsGroup eligible frames back to back -- serial, overlapped, overlapped, serial, so that the
+    // overlapped primary+shadow frames (launch_render): with RT_PS_PIPELINE auto, six groups of
+    // kPsGroup eligible frames back to back -- serial, 2 in flight, 4, 4, 2, serial, so that the
     // clock ramp of a fresh process cancels -- are timed on the caller's stream (events
-    // pev[2g], pev[2g + 1] around group g); the next frame keeps the faster mode for the
+    // pev[2g], pev[2g + 1] around group g); the next frame keeps the fastest mode for the
     // parameter set
-    int ps_phase = 0;               // 0 .. 4 kPsGroup - 1 timing frames, 4 kPsGroup decide, -1 decided
-    bool ps_use = false;
+    int ps_phase = 0;               // 0 .. 6 kPsGroup - 1 timing frames, 6 kPsGroup decide, -1 decided
+    uint32_t ps_use = 0;            // decided: frames in flight (0 = serial)
     uint64_t ps_last = 0;           // r->frames at the last timing frame (any other frame restarts)
-    bool ps_prev = false;           // the previous eligible frame ran overlapped
-    hipEvent_t pev[8] = {};
+    uint32_t ps_prev = 0;           // frames in flight of the previous eligible frame (0 serial)
+    hipEvent_t pev[12] = {};
     hipEvent_t ps_join = nullptr;   // caller's stream -> overlap stream, on a switch to overlapped
-    float ps_ms[4] = {};
-    // the overlapped frames' per-sample results, frame n in buffer n % ps_buffers (kernel on
-    // renderer stream n % 2): frame n + ps_buffers waits for the finishing pass of frame n only,
-    // so a kernel never waits for the finish of the frame just before the one running beside it
-    float4 *ps_res[4] = {};
-    size_t ps_res_bytes[4] = {};
-    hipEvent_t ps_fin[4] = {};
-    bool ps_fin_set[4] = {};
+    float ps_ms[6] = {};
+    // the overlapped frames' per-sample results, frame n in buffer n % buffers (kernel on
+    // renderer stream n % depth): frame n + buffers waits for the finishing pass of frame n only,
+    // so a kernel never waits for the finish of a frame still running beside it
+    float4 *ps_res[5] = {};
+    size_t ps_res_bytes[5] = {};
+    hipEvent_t ps_fin[5] = {};
+    bool ps_fin_set[5] = {};
     uint32_t ps_count = 0;
     // per-sample values of sample-split frames (FrameArgs::samples)
     void *d_samples = nullptr;
@@ -615,7 +620,8 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_XCD_ORDER")) s->xcd_order = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_PIPELINE")) s->pt_pipeline = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PS_PIPELINE")) s->ps_pipeline = std::max(-1, std::min(1, std::atoi(e)));
-    if (const char *e = std::getenv("RT_PS_BUFFERS")) s->ps_buffers = (uint32_t)std::max(2, std::min(4, std::atoi(e)));
+    if (const char *e = std::getenv("RT_PS_BUFFERS")) s->ps_buffers = (uint32_t)std::max(2, std::min(5, std::atoi(e)));
+    if (const char *e = std::getenv("RT_PS_DEPTH")) s->ps_depth = (uint32_t)std::max(2, std::min(4, std::atoi(e)));
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
@@ -678,7 +684,7 @@ constexpr int kPtResBuffers = RT_PT_RES_BUFFERS;   // 2 or 3
 // The renderer's two overlap streams and their ordering events (created once).
 int ensure_pipe_streams(rt_renderer *r) {
     if (r->pt_stream[0]) return RT_OK;
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < 4; ++k) {
         HIP_TRY(hipStreamCreateWithFlags(&r->pt_stream[k], hipStreamNonBlocking));
         // ordering between streams of this device only: a device-scope release
         HIP_TRY(hipEventCreateWithFlags(&r->pt_lv[k], hipEventDisableTiming | hipEventReleaseToDevice));
@@ -929,6 +935,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
     if (key != r->order_key || n != r->order_n) {
         r->order_key = key;
         r->order_state = 0;
+        r->host_cost.clear();
         r->ps_phase = 0;   // the overlap decision belongs to the parameter set too
         if (n != r->order_n) {
             HIP_TRY(hipDeviceSynchronize());                             // frames may still read them
@@ -958,6 +965,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
         HIP_TRY(hipDeviceSynchronize());
         std::vector<uint32_t> cost(n), ord(n);
         HIP_TRY(hipMemcpy(cost.data(), r->d_cost + (size_t)use * n, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        r->host_cost = cost;
         for (uint32_t i = 0; i < n; ++i) ord[i] = i;
         std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
 
@@ -1145,50 +1153,62 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     // It pays where a frame is latency- or tail-bound (mig29 x16 1080p 0.41 -> 0.33 ms, 720p
     // 0.385 -> 0.255 ms) and costs where it is issue-bound (TEAPOT-F 1080p 0.1024 -> 0.1055 ms:
     // the finishing pass's extra 66 MB of sample traffic is not hidden there), and only
-    // when the caller submits frames back to back -- so by default each renderer times both
-    // modes on its own frames and keeps the faster (RT_PS_PIPELINE: -1 auto, 0 off, 1 on).
+    // when the caller submits frames back to back.  A small frame -- a multi-GPU rank's 1/N
+    // shard, about one round of resident waves -- is one latency chain long, and more frames
+    // in flight keep filling its idle issue slots: up to 4 renderer streams (round 3).  So by
+    // default each renderer times serial, 2 and 4 frames in flight on its own frames and keeps
+    // the fastest (RT_PS_PIPELINE: -1 auto, 0 off, 1 on with RT_PS_DEPTH frames in flight).
     const uint64_t ps_bytes = (uint64_t)p->spp * F.ntiles_local * 64u * 16u;
     // (sample-split frames -- a multi-GPU rank's shard at spp N -- store their samples anyway;
     // overlapped, they go to the result buffers instead of d_samples)
     const bool ps_ok = s->ps_pipeline != 0 && mode == RT_MODE_PATH && md == 1 && lds_kind == 0 &&
                        timed < 0 && split_timed < 0 && !F.tile_cost && !walk_pending && ps_bytes <= (2ull << 30);
-    bool ps_pipe = ps_ok && s->ps_pipeline == 1;
+    // frames in flight for this frame: 0 = serial, else 2..4 renderer streams
+    uint32_t depth_k = (ps_ok && s->ps_pipeline == 1) ? s->ps_depth : 0u;
     int ps_ev0 = -1, ps_ev1 = -1;   // pev recorded on the caller's stream before / after this frame
     if (ps_ok && s->ps_pipeline < 0) {
         constexpr int G = kPsGroup;
-        if (r->ps_phase > 0 && r->ps_phase < 4 * G && r->frames != r->ps_last + 1) r->ps_phase = 0;   // interrupted
-        if (r->ps_phase == 4 * G) {
-            HIP_TRY(hipEventSynchronize(r->pev[7]));
-            for (int g = 0; g < 4; ++g) HIP_TRY(hipEventElapsedTime(&r->ps_ms[g], r->pev[2 * g], r->pev[2 * g + 1]));
-            r->ps_use = r->ps_ms[1] + r->ps_ms[2] < r->ps_ms[0] + r->ps_ms[3];
+        static constexpr uint32_t kGroupDepth[6] = {0, 2, 4, 4, 2, 0};
+        if (r->ps_phase > 0 && r->ps_phase < 6 * G && r->frames != r->ps_last + 1) r->ps_phase = 0;   // interrupted
+        if (r->ps_phase == 6 * G) {
+            HIP_TRY(hipEventSynchronize(r->pev[11]));
+            for (int g = 0; g < 6; ++g) HIP_TRY(hipEventElapsedTime(&r->ps_ms[g], r->pev[2 * g], r->pev[2 * g + 1]));
+            const float t0 = r->ps_ms[0] + r->ps_ms[5], t2 = r->ps_ms[1] + r->ps_ms[4], t4 = r->ps_ms[2] + r->ps_ms[3];
+            r->ps_use = (t4 < t2 && t4 < t0) ? 4u : (t2 < t0 ? 2u : 0u);
             r->ps_phase = -1;
         }
         if (r->ps_phase >= 0) {
-            if (r->ps_phase == 0) {   // streams, events and both result buffers before the timing
+            if (r->ps_phase == 0) {   // streams, events and every result buffer before the timing
                 if (!r->pev[0])
                     for (auto &e : r->pev) HIP_TRY(hipEventCreate(&e));
                 int rc = ensure_pipe_streams(r);
-                for (uint32_t k = 0; k < s->ps_buffers && rc == RT_OK; ++k) rc = ensure_ps_res(r, k, ps_bytes);
+                const uint32_t nb = s->ps_buffers ? s->ps_buffers : 5u;
+                for (uint32_t k = 0; k < nb && rc == RT_OK; ++k) rc = ensure_ps_res(r, k, ps_bytes);
                 if (rc != RT_OK) return rc;
             }
-            const int g = r->ps_phase / G;   // serial, overlapped, overlapped, serial
-            ps_pipe = g == 1 || g == 2;
+            const int g = r->ps_phase / G;   // serial, 2, 4, 4, 2, serial frames in flight
+            depth_k = kGroupDepth[g];
             if (r->ps_phase % G == 0) ps_ev0 = 2 * g;
             if (r->ps_phase % G == G - 1) ps_ev1 = 2 * g + 1;
             r->ps_last = r->frames;
             ++r->ps_phase;
         } else {
-            ps_pipe = r->ps_use;
+            depth_k = r->ps_use;
         }
     }
+    const bool ps_pipe = depth_k > 0;
     if (ps_ev0 >= 0) HIP_TRY(hipEventRecord(r->pev[ps_ev0], st));
     uint32_t buf = 0;
     int lane_st = 0;
     if (ps_pipe) {
         int rc = ensure_pipe_streams(r);
         if (rc != RT_OK) return rc;
-        buf = r->ps_count % s->ps_buffers;
-        lane_st = (int)(r->ps_count & 1u);
+        // frame n's kernel on renderer stream n % depth, its samples in buffer n % buffers: with
+        // depth + 1 buffers frame n + depth + 1 waits for frame n's finishing pass only, which
+        // follows frame n's kernel alone -- never a kernel still running beside it
+        const uint32_t buffers = s->ps_buffers ? s->ps_buffers : depth_k + 1u;
+        buf = r->ps_count % buffers;
+        lane_st = (int)(r->ps_count % depth_k);
         ++r->ps_count;
         if ((rc = ensure_ps_res(r, buf, ps_bytes)) != RT_OK) return rc;
         L.stream = r->pt_stream[lane_st];
@@ -1200,7 +1220,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         }
         F.samples = r->ps_res[buf];
     }
-    if (ps_ok) r->ps_prev = ps_pipe;
+    if (ps_ok) r->ps_prev = depth_k;
     if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed], st));
     if (split_timed >= 0) HIP_TRY(hipEventRecord(r->sev[2 * split_timed], st));
     if (s->ext) kext::launch_frame(view, F, L);
@@ -1467,8 +1487,9 @@ int rt_renderer_destroy(rt_renderer *r) {
     (void)hipFree(r->d_acc);
     (void)hipFree(r->d_counters);
     if (r->d_rgb) (void)hipFree(r->d_rgb);
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < 2; ++k)
         if (r->d_pt[k]) (void)hipFree(r->d_pt[k]);
+    for (int k = 0; k < 4; ++k) {
         if (r->pt_stream[k]) (void)hipStreamDestroy(r->pt_stream[k]);
         if (r->pt_lv[k]) (void)hipEventDestroy(r->pt_lv[k]);
     }
@@ -1487,7 +1508,7 @@ int rt_renderer_destroy(rt_renderer *r) {
     for (auto &e : r->pev)
         if (e) (void)hipEventDestroy(e);
     if (r->ps_join) (void)hipEventDestroy(r->ps_join);
-    for (int b = 0; b < 4; ++b) {
+    for (int b = 0; b < 5; ++b) {
         if (r->ps_res[b]) (void)hipFree(r->ps_res[b]);
         if (r->ps_fin[b]) (void)hipEventDestroy(r->ps_fin[b]);
     }
@@ -1554,10 +1575,33 @@ int rt_renderer_counters(rt_renderer *r, rt_counters *out) {
 
 int rt_renderer_overlap(const rt_renderer *r, int *state, float ms[4]) {
     if (!r || !state) return fail(RT_ERR_INVALID, "rt_renderer_overlap: null argument");
+    int depth = 0;
+    float all[6];
+    rt_renderer_overlap_depth(r, &depth, all);
+    *state = depth < 0 ? -1 : (depth > 1 ? 1 : 0);
+    if (ms) {   // serial, 2 in flight, 2 in flight, serial: the groups of the two-mode decision
+        const int g[4] = {0, 1, 4, 5};
+        for (int k = 0; k < 4; ++k) ms[k] = all[g[k]];
+    }
+    return RT_OK;
+}
+
+int rt_renderer_overlap_depth(const rt_renderer *r, int *depth, float ms[6]) {
+    if (!r || !depth) return fail(RT_ERR_INVALID, "rt_renderer_overlap_depth: null argument");
     const int32_t mode = r->scene->ps_pipeline;
-    *state = mode >= 0 ? mode : (r->ps_phase == -1 ? (r->ps_use ? 1 : 0) : -1);
+    const bool decided = mode < 0 && r->ps_phase == -1;
+    if (mode == 0) *depth = 1;
+    else if (mode == 1) *depth = (int)r->scene->ps_depth;
+    else *depth = decided ? (r->ps_use ? (int)r->ps_use : 1) : -1;
     if (ms)
-        for (int g = 0; g < 4; ++g) ms[g] = (mode < 0 && r->ps_phase == -1) ? r->ps_ms[g] : 0.0f;
+        for (int g = 0; g < 6; ++g) ms[g] = decided ? r->ps_ms[g] : 0.0f;
+    return RT_OK;
+}
+
+int rt_renderer_tile_costs(const rt_renderer *r, uint32_t *costs, uint32_t n, uint32_t *n_out) {
+    if (!r || !n_out || (n && !costs)) return fail(RT_ERR_INVALID, "rt_renderer_tile_costs: null argument");
+    *n_out = (uint32_t)r->host_cost.size();
+    if (n && !r->host_cost.empty()) std::memcpy(costs, r->host_cost.data(), sizeof(uint32_t) * std::min<size_t>(n, r->host_cost.size()));
     return RT_OK;
 }
 

@@ -554,6 +554,23 @@ static int mesh_read(const std::string &path, std::vector<float> &V, std::vector
     return RT_OK;
 }
 
+// tinyobj-compatible OBJ read (Scene::LoadModel's LoadObj, template/scene.h:156-161)
+static int obj_read(const std::string &path, std::vector<float> &V, std::vector<int32_t> &F) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) return fail(RT_ERR_IO, "cannot open " + path);
+    obj::Reader rd;
+    std::string line;
+    size_t lineno = 0;
+    while (std::getline(in, line)) {   // '\n' lines; the trailing '\r' of CRLF is dropped
+        ++lineno;
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        if (rd.line(line) != 0) return fail(RT_ERR_IO, "bad face at line " + std::to_string(lineno) + " of " + path);
+    }
+    V.swap(rd.v);
+    F.swap(rd.f);
+    return RT_OK;
+}
+
 static void append_mesh(const std::vector<float> &V, const std::vector<int32_t> &F, const float M[16], int32_t mat,
                         std::vector<rt_prim> &out) {
     size_t nt = F.size() / 3;
@@ -601,7 +618,9 @@ int recipe_source(const std::string &name, const std::string &dir, SceneSource &
     auto mesh = [&](const char *file, const float M[16], int32_t mat) {
         std::vector<float> V;
         std::vector<int32_t> F;
-        int rc = mesh_read(dir + "/" + file + ".rtmesh", V, F);
+        // the bundled RTMESH1 file, or the reference's own assets/<file>.obj in that directory
+        const std::string base = dir + "/" + file;
+        int rc = std::ifstream(base + ".rtmesh").good() ? mesh_read(base + ".rtmesh", V, F) : obj_read(base + ".obj", V, F);
         if (rc == RT_OK) append_mesh(V, F, M, mat, out.prims);
         return rc;
     };
@@ -620,7 +639,7 @@ int recipe_source(const std::string &name, const std::string &dir, SceneSource &
     int32_t white = material(RT_DIFFUSE, mk(0.95f, 0.95f, 0.95f));       // scene.h:46
     int32_t green = material(RT_DIFFUSE, mk(0.05f, 0.95f, 0.05f));       // scene.h:44
     int32_t check = material(RT_CHECKERBOARD, mk(0.1f, 0.1f, 0.1f), mk(0.9f, 0.9f, 0.9f));   // scene.h:50
-    bool high_light = (name == "teapot" || name == "mig16");
+    bool high_light = (name == "teapot" || name == "mig16" || name == "default");
     sphere(high_light ? mk(0.0f, 6.0f, 5.0f) : mk(0.0f, 4.0f, -2.0f), 0.5f, lamp);
 
     float T[16], R[16], R2[16], R3[16], S[16], M[16];
@@ -657,6 +676,23 @@ int recipe_source(const std::string &name, const std::string &dir, SceneSource &
             rc = mesh("glider", M, mirror);
         }
         floor2(check);
+    } else if (name == "default") {
+        // the reference's as-shipped Scene() (template/scene.h:40-128): light (0,6,5), then
+        // cloud.obj, airways.obj, glider, piper_pa18.obj, mig29 -- cloud, airways and piper are
+        // not in assets/, and LoadModel returns without triangles for them (scene.h:164-168)
+        int32_t red = material(RT_DIFFUSE, mk(0.95f, 0.05f, 0.05f));     // scene.h:43
+        translate_matrix(1.0f, 0.0f, 0.0f, T);                            // scene.h:88
+        mat_rotate(2, -0.15f * kPI, R); mat_rotate(1, 0.05f * kPI, R2); mat_rotate(0, -0.55f * kPI, R3);
+        identity(S); S[0] = S[5] = S[10] = 0.025f;
+        chain({T, R, R2, R3, S}, M);
+        rc = mesh("glider", M, red);
+        if (rc == RT_OK) {                                                // scene.h:94
+            translate_matrix(0.1f, 0.2f, -0.2f, T);
+            mat_rotate(2, 1.1f * kPI, R); mat_rotate(1, 0.05f * kPI, R2); mat_rotate(0, 0.2f * kPI, R3);
+            identity(S); S[0] = S[5] = S[10] = 0.001f;
+            chain({T, R, R2, R3, S}, M);
+            rc = mesh("mig29", M, green);
+        }
     } else if (name == "cfg5") {
         translate_matrix(0, -1.2f, 2.5f, T);
         identity(S); S[0] = S[5] = S[10] = 12.0f;
@@ -682,22 +718,16 @@ void rt_free(void *p) { std::free(p); }
 
 int rt_obj_load(const char *path, float **verts, uint32_t *nv, int32_t **faces, uint32_t *nt) {
     if (!path || !verts || !nv || !faces || !nt) return fail(RT_ERR_INVALID, "rt_obj_load: null argument");
-    std::ifstream in(path, std::ios::binary);
-    if (!in) return fail(RT_ERR_IO, std::string("cannot open ") + path);
-    obj::Reader rd;
-    std::string line;
-    size_t lineno = 0;
-    while (std::getline(in, line)) {   // '\n' lines; the trailing '\r' of CRLF is skipped by the tokenizer
-        ++lineno;
-        if (!line.empty() && line.back() == '\r') line.pop_back();
-        if (rd.line(line) != 0) return fail(RT_ERR_IO, "bad face at line " + std::to_string(lineno) + " of " + path);
-    }
-    *nv = (uint32_t)(rd.v.size() / 3);
-    *nt = (uint32_t)(rd.f.size() / 3);
-    *verts = static_cast<float *>(std::malloc(sizeof(float) * (rd.v.size() ? rd.v.size() : 1)));
-    *faces = static_cast<int32_t *>(std::malloc(sizeof(int32_t) * (rd.f.size() ? rd.f.size() : 1)));
-    std::memcpy(*verts, rd.v.data(), sizeof(float) * rd.v.size());
-    std::memcpy(*faces, rd.f.data(), sizeof(int32_t) * rd.f.size());
+    std::vector<float> V;
+    std::vector<int32_t> F;
+    int rc = obj_read(path, V, F);
+    if (rc != RT_OK) return rc;
+    *nv = (uint32_t)(V.size() / 3);
+    *nt = (uint32_t)(F.size() / 3);
+    *verts = static_cast<float *>(std::malloc(sizeof(float) * (V.size() ? V.size() : 1)));
+    *faces = static_cast<int32_t *>(std::malloc(sizeof(int32_t) * (F.size() ? F.size() : 1)));
+    std::memcpy(*verts, V.data(), sizeof(float) * V.size());
+    std::memcpy(*faces, F.data(), sizeof(int32_t) * F.size());
     return RT_OK;
 }
 

@@ -45,9 +45,20 @@ const Rccl &rccl() {
     static Rccl R;
     static std::once_flag once;
     std::call_once(once, [] {
+        // RT_RCCL_LIB: a library with RCCL's point-to-point API to use instead -- the tests'
+        // in-process stand-in (tests/cpp/inproc_rccl.cpp) that runs several ranks as threads of
+        // one process on one GPU, which RCCL itself refuses
+        if (const char *e = std::getenv("RT_RCCL_LIB")) {
+            R.h = dlopen(e, RTLD_NOW | RTLD_LOCAL);
+            if (!R.h) {
+                const char *d = dlerror();
+                R.error = std::string("RT_RCCL_LIB not loadable: ") + (d ? d : e);
+                return;
+            }
+        }
         for (const char *name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
-            R.h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
             if (R.h) break;
+            R.h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
         }
         if (!R.h) {
             const char *e = dlerror();
@@ -104,6 +115,8 @@ struct rt_comm {
     uint32_t *gathered[2] = {nullptr, nullptr};   // rank 0: world x cap, slot 0 rendered in place
     hipEvent_t ev_render[2] = {nullptr, nullptr}, ev_gather[2] = {nullptr, nullptr};
     hipEvent_t ev_asm[2] = {nullptr, nullptr};   // rank 0, pipelined: frame assembled (comm stream)
+    hipEvent_t ev_caller = nullptr;        // rank 0, pipelined: the caller's stream at the call, so the
+                                           // unshuffle into rgb8_dev follows the caller's reads of it
     int slot = 0;
     int pending = -1;                      // slot whose gather is in flight (pipelined mode)
     uint64_t frames = 0;
@@ -261,6 +274,7 @@ int rt_comm_destroy(rt_comm *c) {
         if (c->ev_gather[k]) (void)hipEventDestroy(c->ev_gather[k]);
         if (c->ev_asm[k]) (void)hipEventDestroy(c->ev_asm[k]);
     }
+    if (c->ev_caller) (void)hipEventDestroy(c->ev_caller);
     for (auto &e : c->tev)
         for (auto &x : e) (void)hipEventDestroy(x);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
@@ -273,10 +287,31 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
                           uint32_t *rgb8_dev, uint32_t flags, void *stream) {
     if (!r || !c || !cam || !p) return fail(RT_ERR_INVALID, "rt_render_frame_multi: null argument");
     if (flags & ~(uint32_t)(RT_MULTI_PIPELINED | RT_MULTI_TIMING)) return fail(RT_ERR_INVALID, "rt_render_frame_multi: unknown flags");
+    const bool pipelined = (flags & RT_MULTI_PIPELINED) != 0;
+    // every check before the first side effect: a rejected call leaves the accumulator, the
+    // frame count and the communicator as they were
+    if (!pipelined && c->pending >= 0)
+        return fail(RT_ERR_INVALID, "rt_render_frame_multi: a pipelined frame is pending (rt_multi_flush)");
+    if (c->rank == 0 && !rgb8_dev && (!pipelined || c->pending >= 0))
+        return fail(RT_ERR_INVALID, "rt_render_frame_multi: rank 0 needs an output frame");
     HIP_TRY(hipSetDevice(c->device));
     int rc = bind_renderer(c, r);
     if (rc != RT_OK) return rc;
     hipStream_t st = (hipStream_t)stream;
+    if (pipelined && !c->comm_stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+        for (int j = 0; j < 2; ++j) {
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_render[j], sync_event_flags()));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_gather[j], sync_event_flags()));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_asm[j], sync_event_flags()));
+        }
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_caller, sync_event_flags()));
+    }
+    // rank 0, pipelined: this call unshuffles the previous frame into rgb8_dev on the
+    // communicator's stream; whatever the caller queued on its stream before this call (a copy
+    // or display of the frame before) must be done with rgb8_dev first
+    const bool assemble_prev = pipelined && c->rank == 0 && c->pending >= 0;
+    if (assemble_prev) HIP_TRY(hipEventRecord(c->ev_caller, st));
     const int k = c->slot;
     uint32_t *mine = c->rank == 0 ? c->gathered[k] : c->tiles[k];
     std::array<hipEvent_t, 3> *tv = nullptr;
@@ -292,8 +327,7 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
     rc = rt_render_shard(r, cam, p, (uint32_t)c->rank, (uint32_t)c->world, mine, st);
     if (rc != RT_OK) return rc;
     if (tv) HIP_TRY(hipEventRecord((*tv)[1], st));
-    if (!(flags & RT_MULTI_PIPELINED)) {
-        if (c->pending >= 0) return fail(RT_ERR_INVALID, "rt_render_frame_multi: a pipelined frame is pending (rt_multi_flush)");
+    if (!pipelined) {
         if ((rc = gather(c, k, st)) != RT_OK) return rc;   // in stream order after the render
         if (tv) HIP_TRY(hipEventRecord((*tv)[2], st));
         if ((rc = assemble(c, r, k, rgb8_dev, st)) != RT_OK) return rc;
@@ -304,21 +338,13 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
     // stream goes on (the next frame's render).  The previous frame is completed here: on rank
     // 0 its unshuffle also runs on the communicator's stream, right behind its gather, so the
     // render stream does not wait for it (only the render into its slot, one frame later, does)
-    if (!c->comm_stream) {
-        HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
-        for (int j = 0; j < 2; ++j) {
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_render[j], sync_event_flags()));
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_gather[j], sync_event_flags()));
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_asm[j], sync_event_flags()));
-        }
-    }
     if (c->pending >= 0) {
-        // frame i-1: assembled after its gather (stream order on the comm stream); its buffers
-        // are rendered into again by the next call, which the render stream reaches only after
-        // this wait
+        // frame i-1: assembled after its gather (stream order on the comm stream) and after the
+        // caller's earlier work on rgb8_dev; its buffers are rendered into again by the next
+        // call, which the render stream reaches only after this wait
         const int j = c->pending;
         if (c->rank == 0) {
-            if (!rgb8_dev) return fail(RT_ERR_INVALID, "rt_render_frame_multi: rank 0 needs an output frame");
+            HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_caller, 0));
             if ((rc = assemble(c, r, j, rgb8_dev, c->comm_stream)) != RT_OK) return rc;
             HIP_TRY(hipEventRecord(c->ev_asm[j], c->comm_stream));
             HIP_TRY(hipStreamWaitEvent(st, c->ev_asm[j], 0));

@@ -169,7 +169,10 @@ int rt_image_load(const char *path, uint32_t **pixels, uint32_t *width, uint32_t
 
 /* ---- scene (Scene, template/scene.h:37-1014) ------------------------------ */
 int rt_scene_create(const rt_scene_desc *desc, rt_scene **out);
-/* the SURVEY.md 8(d) scenes: "teapotF", "teapot", "mig16", "cfg3", "cfg5" */
+/* the SURVEY.md 8(d) scenes: "teapotF", "teapot", "mig16", "cfg3", "cfg5"; and "default", the
+ * reference's as-shipped Scene() (template/scene.h:40-128: light, glider, mig29 -- the other
+ * models it names are not in its assets/).  mesh_dir holds <name>.rtmesh or the reference's
+ * <name>.obj files. */
 int rt_scene_create_recipe(const char *name, const char *mesh_dir, int32_t device, rt_scene **out);
 /* the same with the BVH kind chosen (RT_BVH_PLAIN / RT_BVH_SBVH) */
 int rt_scene_create_recipe_ex(const char *name, const char *mesh_dir, int32_t device, int32_t bvh_kind, rt_scene **out);
@@ -281,9 +284,20 @@ int rt_renderer_counters(rt_renderer *r, rt_counters *out);
  * renderer.cpp:200-309, is one serial pass): *state = 1 this renderer's primary+shadow frames
  * run overlapped (frame kernel on a renderer stream, accumulate + RGB8 in a finishing pass on
  * the caller's stream), 0 serial, -1 not decided yet (RT_PS_PIPELINE=-1 times both modes on
- * the first eligible frames); ms (may be NULL) = the four timed groups' milliseconds (serial,
- * overlapped, overlapped, serial) when decided by timing, else zeros. */
+ * the first eligible frames); ms (may be NULL) = the serial and 2-in-flight groups' milliseconds
+ * (serial, overlapped, overlapped, serial) when decided by timing, else zeros. */
 int rt_renderer_overlap(const rt_renderer *r, int *state, float ms[4]);
+/* The same decision with its depth: *depth = primary+shadow frames in flight (1 serial, 2..4
+ * overlapped on that many renderer streams; -1 not decided yet).  RT_PS_PIPELINE=-1 times six
+ * groups of eight frames -- serial, 2, 4, 4, 2, serial in flight -- and keeps the fastest;
+ * RT_PS_PIPELINE=1 forces RT_PS_DEPTH (default 2).  ms (may be NULL) = the six groups' ms. */
+int rt_renderer_overlap_depth(const rt_renderer *r, int *depth, float ms[6]);
+/* The measured cost map behind the longest-tile-first order of the renderer's current parameter
+ * set (camera, size, spp, depth, mode, shard): costs[i] = wave cycles (s_memtime ticks) of
+ * local tile i, recorded on one frame; *n_out = its tile count (0 until recorded: from the 2nd
+ * frame of a parameter set on).  At most n entries are copied.  Diagnostics and cost-balanced
+ * tile deals. */
+int rt_renderer_tile_costs(const rt_renderer *r, uint32_t *costs, uint32_t n, uint32_t *n_out);
 /* accumulator readback, W*H float4 */
 int rt_renderer_read_accumulator(rt_renderer *r, float *host_out);
 /* Name of the frame kernel rt_render_frame / rt_render_shard launch for these params

@@ -1720,7 +1720,7 @@ or_scene *or_scene_recipe(const char *name, const char *dir) {
     int mwhite = or_scene_add_material(s, OR_DIFFUSE, white, NULL, 0, 0);       /* scene.h:46 */
     int mgreen = or_scene_add_material(s, OR_DIFFUSE, green, NULL, 0, 0);       /* scene.h:44 */
     int mcheck = or_scene_add_material(s, OR_CHECKER, ck1, ck2, 0, -1.0f);      /* scene.h:50 */
-    int teapot_like = !strcmp(name, "teapot") || !strcmp(name, "mig16");
+    int teapot_like = !strcmp(name, "teapot") || !strcmp(name, "mig16") || !strcmp(name, "default");
     float lp[3] = {0.0f, teapot_like ? 6.0f : 4.0f, teapot_like ? 5.0f : -2.0f};
     or_scene_add_sphere(s, lp, 0.5f, lamp);
     float T[16], R[16], S[16], R2[16], R3[16], M[16];
@@ -1756,6 +1756,22 @@ or_scene *or_scene_recipe(const char *name, const char *dir) {
         const float *c2[5] = {T, R, R2, R3, S}; chain(M, c2, 5);
         rc |= add_mesh_file(s, dir, "glider", M, mirror);
         floor2(s, mcheck);
+    } else if (!strcmp(name, "default")) {
+        /* the reference's as-shipped Scene() (template/scene.h:40-128): light (0,6,5), then
+           cloud.obj, airways.obj, glider, piper_pa18.obj, mig29 -- cloud, airways and piper are
+           not in assets/, and LoadModel returns without triangles for them (scene.h:164-168) */
+        const float red[3] = {0.95f, 0.05f, 0.05f};
+        int mred = or_scene_add_material(s, OR_DIFFUSE, red, NULL, 0, 0);       /* scene.h:43 */
+        or_mat4_translate(T, 1.0f, 0.0f, 0.0f);                                   /* scene.h:88 */
+        or_mat4_rotate_z(R, -0.15f * PI_F); or_mat4_rotate_y(R2, 0.05f * PI_F); or_mat4_rotate_x(R3, -0.55f * PI_F);
+        or_mat4_scale(S, 0.025f);
+        const float *c2[5] = {T, R, R2, R3, S}; chain(M, c2, 5);
+        rc |= add_mesh_file(s, dir, "glider", M, mred);
+        or_mat4_translate(T, 0.1f, 0.2f, -0.2f);                                  /* scene.h:94 */
+        or_mat4_rotate_z(R, 1.1f * PI_F); or_mat4_rotate_y(R2, 0.05f * PI_F); or_mat4_rotate_x(R3, 0.2f * PI_F);
+        or_mat4_scale(S, 0.001f);
+        const float *c3[5] = {T, R, R2, R3, S}; chain(M, c3, 5);
+        rc |= add_mesh_file(s, dir, "mig29", M, mgreen);
     } else if (!strcmp(name, "cfg5")) {
         or_mat4_translate(T, 0, -1.2f, 2.5f); or_mat4_scale(S, 12.0f);
         const float *c[2] = {T, S}; chain(M, c, 2);

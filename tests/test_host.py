@@ -60,6 +60,35 @@ def test_compat_header_compiles(rt, tmp_path):
         assert r.returncode == 0, r.stdout
 
 
+def test_reference_shaped_host(rt):
+    """tests/cpp/reference_main.cpp: the reference's main (template/template.cpp:133-139, 269-287)
+    and float3 math with only `#include "precomp.h"` swapped for rt_compat.hpp -- Surface,
+    `new Renderer()`, Init, Tick(float), the K key, Shutdown; the default scene from the bundled
+    meshes.  Without a GPU it must stop with RT_ERR_NO_DEVICE (exit 3) after the host-side
+    checks passed; with one, frames come back (exit 0)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp"), "reference_main"], check=True)
+    env = dict(os.environ, RT_MESH_DIR=rt.DATA_DIR)
+    r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "reference_main")], capture_output=True, text=True, env=env)
+    assert r.returncode == (3 if rt.device_count() == 0 else 0), r.stdout + r.stderr
+
+
+def test_default_recipe_from_reference_assets(rt, oracle, reference_assets):
+    """Recipe "default" = the reference's as-shipped Scene() (template/scene.h:40-128): read from
+    the reference's own assets/*.obj (the recipe loader falls back to OBJ files) it equals the
+    bundled-mesh recipe bit for bit, and its plain BVH equals the oracle's."""
+    pa, ma = rt.recipe_describe("default")
+    pb, mb = rt.recipe_describe("default", mesh_dir=reference_assets)
+    raw = lambda xs: b"".join(bytes(x) for x in xs)
+    assert len(pa) == 1 + 21364 + 6546 and raw(pa) == raw(pb) and raw(ma) == raw(mb)
+    nodes, idx, info = rt.build_bvh_host(pa)
+    o = oracle.Scene("default", rt.DATA_DIR)
+    on = o.nodes().copy()
+    nodes = nodes.copy()
+    on[1] = 0
+    nodes[1] = 0
+    assert info["nodes_used"] == o.nodes_used and np.array_equal(nodes, on) and np.array_equal(idx, o.indices())
+
+
 def test_abi_version_and_device_count(rt):
     assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 3
     assert rt.device_count() >= 0

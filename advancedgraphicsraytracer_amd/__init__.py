@@ -24,7 +24,7 @@ HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "rt_amd.h")
 ABI_VERSION = 3   # include/rt_amd.h RT_ABI_VERSION
 RT_OK, RT_ERR_INVALID, RT_ERR_NO_DEVICE, RT_ERR_HIP, RT_ERR_IO, RT_ERR_UNSUPPORTED, RT_ERR_COMM = 0, -1, -2, -3, -4, -5, -6
 RT_COMM_ID_BYTES = 128
-MULTI_PIPELINED, MULTI_TIMING = 1, 2
+MULTI_PIPELINED, MULTI_TIMING, MULTI_BALANCED = 1, 2, 4
 SPHERE, PLANE, CUBE, QUAD, TRIANGLE = 0, 1, 2, 3, 4
 DIFFUSE, MIRROR, DIELECTRIC, CHECKERBOARD, LIGHT, DSMIX, TEXTURE = 0, 1, 2, 3, 4, 5, 6
 MODE_PATH = 0
@@ -157,6 +157,9 @@ def lib():
         "rt_shard_capacity": ([u32, u32, u32, C.POINTER(u32)], C.c_int),
         "rt_render_shard": ([vp, C.POINTER(Camera), C.POINTER(FrameParams), u32, u32, vp, vp], C.c_int),
         "rt_assemble_shards": ([vp, vp, u32, vp, vp], C.c_int),
+        "rt_tile_deal": ([u32, u32, C.POINTER(u32), u32, C.POINTER(u32), C.POINTER(u32)], C.c_int),
+        "rt_render_shard_tiles": ([vp, C.POINTER(Camera), C.POINTER(FrameParams), C.POINTER(u32), u32, vp, vp], C.c_int),
+        "rt_assemble_tiles": ([vp, vp, u32, C.POINTER(u32), C.POINTER(u32), u32, vp, vp], C.c_int),
         "rt_renderer_counters": ([vp, C.POINTER(Counters)], C.c_int),
         "rt_renderer_read_accumulator": ([vp, fp], C.c_int),
         "rt_renderer_overlap": ([vp, C.POINTER(C.c_int), fp], C.c_int),
@@ -362,6 +365,21 @@ def quad(size, material, T=None):
     p.v[0] = size
     p.T = None if T is None else np.asarray(T, np.float32).reshape(16)
     return p
+
+
+def tile_deal(width, height, num_shards, cost=None):
+    """rt_tile_deal: (deal_tiles[ntiles], deal_off[num_shards + 1]) -- the Morton-ordered 8x8
+    tiles cut into runs of equal summed cost (cost[t] per global tile; None = equal)."""
+    n = ((width + 7) // 8) * ((height + 7) // 8)
+    tiles, off = np.zeros(n, np.uint32), np.zeros(num_shards + 1, np.uint32)
+    cp = None
+    if cost is not None:
+        c = np.ascontiguousarray(cost, np.uint32)
+        assert len(c) == n
+        cp = c.ctypes.data_as(C.POINTER(C.c_uint32))
+    _check(lib().rt_tile_deal(width, height, cp, num_shards, tiles.ctypes.data_as(C.POINTER(C.c_uint32)),
+                              off.ctypes.data_as(C.POINTER(C.c_uint32))))
+    return tiles, off
 
 
 def load_image(path):
@@ -642,6 +660,29 @@ class Renderer:
                                       C.c_void_p(out.data_ptr()), C.c_void_p(s)))
         if frame is None:
             self.frame += 1
+        return out
+
+    def render_shard_tiles(self, out, tiles, spp=1, depth=None, frame=None, reset=False, stream=None):
+        """rt_render_shard_tiles: the listed global tiles (an explicit deal's share), packed [i][64]."""
+        torch = _torch()
+        p = self.params(spp, depth, frame, reset)
+        t = np.ascontiguousarray(tiles, np.uint32)
+        s = stream if stream is not None else torch.cuda.current_stream(out.device).cuda_stream
+        _check(self.L.rt_render_shard_tiles(self.h, C.byref(self.camera), C.byref(p), t.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                            len(t), C.c_void_p(out.data_ptr()), C.c_void_p(s)))
+        if frame is None:
+            self.frame += 1
+        return out
+
+    def assemble_tiles(self, gathered, stride_px, deal_tiles, deal_off, out, stream=None):
+        """rt_assemble_tiles: shard k's packed tiles at gathered[k * stride_px:] -> out (row-major)."""
+        torch = _torch()
+        dt = np.ascontiguousarray(deal_tiles, np.uint32)
+        do = np.ascontiguousarray(deal_off, np.uint32)
+        s = stream if stream is not None else torch.cuda.current_stream(out.device).cuda_stream
+        _check(self.L.rt_assemble_tiles(self.h, C.c_void_p(gathered.data_ptr()), stride_px,
+                                        dt.ctypes.data_as(C.POINTER(C.c_uint32)), do.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                        len(do) - 1, C.c_void_p(out.data_ptr()), C.c_void_p(s)))
         return out
 
     def assemble(self, gathered, num_shards, out, stream=None):

@@ -61,6 +61,8 @@ struct FrameArgs {
     float lens, rw, rh;
     uint32_t W, H, spp, depth, frame, reset;
     uint32_t shard, nshards, tiles_x, ntiles_local;
+    const uint32_t *tile_map;           // explicit deal: local tile -> global tile (nullptr: the
+                                        // interleaved deal, local * nshards + shard)
     uint32_t nchunks, nunits;           // sample chunks per tile (1 = no split); ntiles_local * nchunks
     float4 *samples;                    // non-null: per-sample values [spp][ntiles_local][64] (sample
                                         // split, overlapped frames); k_pt_finish accumulates them
@@ -151,7 +153,8 @@ struct TraceArgs {
 RT_DECLARE_LAUNCHERS(kcore)
 RT_DECLARE_LAUNCHERS(kext)
 #undef RT_DECLARE_LAUNCHERS
-void launch_assemble(const uint32_t *gathered, uint32_t cap, uint32_t nshards, uint32_t tiles_x, uint32_t ntiles,
-                     uint32_t W, uint32_t H, uint32_t *out, hipStream_t st);
+// where: per global tile (shard << 24 | local tile) of an explicit deal; nullptr = interleaved
+void launch_assemble(const uint32_t *gathered, uint32_t cap, uint32_t nshards, const uint32_t *where, uint32_t tiles_x,
+                     uint32_t ntiles, uint32_t W, uint32_t H, uint32_t *out, hipStream_t st);
 
 }  // namespace rt

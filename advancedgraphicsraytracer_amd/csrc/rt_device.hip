@@ -155,6 +155,15 @@ struct rt_renderer {
     // per-sample values of sample-split frames (FrameArgs::samples)
     void *d_samples = nullptr;
     size_t samples_bytes = 0;
+    // explicit tile deal of rt_render_shard_tiles (FrameArgs::tile_map): local -> global tile,
+    // uploaded when it changes; and rank 0's per-global-tile (shard << 24 | local) for assembly
+    std::vector<uint32_t> map_host;
+    uint32_t *d_map = nullptr;
+    size_t map_cap = 0;
+    uint64_t map_hash = 0;
+    uint32_t *d_where = nullptr;
+    size_t where_cap = 0;
+    uint64_t where_hash = 0;
 };
 
 namespace {
@@ -664,12 +673,46 @@ uint64_t frame_pixels(const rt_renderer *r, const FrameArgs &F, uint32_t shard, 
     uint64_t px = (uint64_t)F.ntiles_local * 64u;
     if ((r->W & 7u) || (r->H & 7u)) {
         px = 0;
-        for (uint32_t t = shard; t < ntiles; t += nshards) {
+        auto add = [&](uint32_t t) {
             uint32_t tx = t % tiles_x, ty = t / tiles_x;
             px += (uint64_t)std::min(8u, r->W - tx * 8) * std::min(8u, r->H - ty * 8);
-        }
+        };
+        if (F.tile_map)
+            for (uint32_t t : r->map_host) add(t);
+        else
+            for (uint32_t t = shard; t < ntiles; t += nshards) add(t);
     }
     return px;
+}
+
+uint64_t fnv1a(const void *d, size_t n, uint64_t h = 1469598103934665603ull) {
+    const unsigned char *c = static_cast<const unsigned char *>(d);
+    for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+    return h;
+}
+
+// an explicit deal's tile list on the device (FrameArgs::tile_map); a changed list waits for
+// every frame still reading the old one
+int set_tile_map(rt_renderer *r, const uint32_t *tiles, uint32_t n, uint32_t ntiles) {
+    const uint64_t h = fnv1a(tiles, sizeof(uint32_t) * n, fnv1a(&n, sizeof(n)));
+    if (r->d_map && h == r->map_hash && r->map_host.size() == n) return RT_OK;
+    std::vector<uint8_t> seen(ntiles, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (tiles[i] >= ntiles || seen[tiles[i]]) return fail(RT_ERR_INVALID, "tile list: index out of range or repeated");
+        seen[tiles[i]] = 1;
+    }
+    HIP_TRY(hipDeviceSynchronize());
+    if (n > r->map_cap || !r->d_map) {
+        if (r->d_map) HIP_TRY(hipFree(r->d_map));
+        r->d_map = nullptr;
+        r->map_cap = 0;
+        HIP_TRY(hipMalloc(&r->d_map, sizeof(uint32_t) * std::max<size_t>(n, 1)));
+        r->map_cap = std::max<size_t>(n, 1);
+    }
+    if (n) HIP_TRY(hipMemcpy(r->d_map, tiles, sizeof(uint32_t) * n, hipMemcpyHostToDevice));
+    r->map_host.assign(tiles, tiles + n);
+    r->map_hash = h;
+    return RT_OK;
 }
 
 
@@ -865,7 +908,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
 // tiles in Morton order holding 1/8 of the measured cost -- costliest tile first.  Each XCD's
 // L2 then holds the nodes of its region only, not of the whole frame.  A group whose region
 // ran out takes tiles from the region with the most cost left.
-std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const std::vector<uint32_t> &entries,
+std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const uint32_t *map, const std::vector<uint32_t> &entries,
                                         const std::vector<uint32_t> &cost) {
     // entries: order entries (local tile | split bits); an entry's cost is its tile's, halved
     // for a half-tile entry (bit 31)
@@ -881,7 +924,7 @@ std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const std::vector<ui
     double total = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t e = entries[i], lt = e & 0x3fffffffu;
-        const uint32_t tile = lt * F.nshards + F.shard;
+        const uint32_t tile = map ? map[lt] : lt * F.nshards + F.shard;
         code[i] = morton(tile % F.tiles_x, tile / F.tiles_x) * 4u + (e >> 30);
         ec[i] = (e >> 31) ? 0.5 * cost[lt] : (double)cost[lt];
         z[i] = i;
@@ -931,6 +974,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
     mix(&p->width, sizeof(uint32_t) * 4);   // width height spp depth
     mix(&p->mode, sizeof(uint32_t));
     mix(&F.shard, sizeof(uint32_t) * 2);    // shard nshards
+    if (F.tile_map) mix(&r->map_hash, sizeof(r->map_hash));   // an explicit deal's tile list
     const uint32_t n = F.ntiles_local;
     if (key != r->order_key || n != r->order_n) {
         r->order_key = key;
@@ -987,8 +1031,9 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
         }
         for (uint32_t i = k; i < n; ++i) sp.push_back(ord[i]);
         if (r->scene->xcd_order && split_ok) {   // both orders grouped by XCD (global-node frame kernel)
-            ent = xcd_grouped_order(F, ord, cost);
-            sp = xcd_grouped_order(F, sp, cost);
+            const uint32_t *map = F.tile_map ? r->map_host.data() : nullptr;
+            ent = xcd_grouped_order(F, map, ord, cost);
+            sp = xcd_grouped_order(F, map, sp, cost);
         }
         ent.insert(ent.end(), sp.begin(), sp.end());
         HIP_TRY(hipMemcpy(r->d_order, ent.data(), ent.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -1019,7 +1064,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
 constexpr int kPsGroup = 8;   // frames per timed group of the overlap decision
 
 int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
-                  uint32_t *out, int packed, void *stream) {
+                  uint32_t *out, int packed, void *stream, const uint32_t *tiles = nullptr, uint32_t ntiles_map = 0) {
     if (!r || !cam || !p || !out) return fail(RT_ERR_INVALID, "rt_render: null argument");
     if (p->width != r->W || p->height != r->H)
         return fail(RT_ERR_INVALID, "frame size differs from the renderer's accumulator");
@@ -1040,6 +1085,12 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     const uint32_t tiles_x = (r->W + 7) / 8, tiles_y = (r->H + 7) / 8, ntiles = tiles_x * tiles_y;
     F.shard = shard; F.nshards = nshards; F.tiles_x = tiles_x;
     F.ntiles_local = shard < ntiles ? (ntiles - shard + nshards - 1) / nshards : 0;
+    if (tiles) {   // an explicit deal (rt_render_shard_tiles)
+        int rc = set_tile_map(r, tiles, ntiles_map, ntiles);
+        if (rc != RT_OK) return rc;
+        F.ntiles_local = ntiles_map;
+        F.tile_map = r->d_map;
+    }
     F.packed_out = packed;
     F.acc = r->d_acc;
     F.out = out;
@@ -1094,6 +1145,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         lds = stack_bytes(s);
     }
     if (wavefront) {
+        r->host_cost.clear();   // no tile costs are measured for wavefront frames
         int rc = launch_pt_frame(r, F, s->view, tex, st);
         if (rc != RT_OK) return rc;
         r->primary += frame_pixels(r, F, shard, nshards, tiles_x, ntiles) * p->spp;
@@ -1252,6 +1304,58 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
 }
 
 }  // namespace
+
+// accumulator <-> packed [tile][64] float4 of listed tiles: one wave per tile, one lane per pixel
+__global__ __launch_bounds__(256) void k_acc_tiles(float4 *__restrict__ acc, float4 *__restrict__ buf,
+                                                   const uint32_t *__restrict__ tiles, uint32_t n, uint32_t tiles_x,
+                                                   uint32_t W, uint32_t H, int unpack) {
+    const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    if (i >= n) return;
+    const uint32_t t = tiles[i];
+    const uint32_t x = (t % tiles_x) * 8u + (lane & 7u), y = (t / tiles_x) * 8u + (lane >> 3);
+    const bool on = x < W && y < H;
+    if (unpack) {
+        if (on) acc[x + (size_t)y * W] = buf[(size_t)i * 64u + lane];
+    } else {
+        buf[(size_t)i * 64u + lane] = on ? acc[x + (size_t)y * W] : make_float4(0, 0, 0, 0);
+    }
+}
+
+int rt::renderer_accumulator(rt_renderer *r, void **acc_dev, size_t *bytes) {
+    if (!r || !acc_dev || !bytes) return fail(RT_ERR_INVALID, "null argument");
+    *acc_dev = r->d_acc;
+    *bytes = sizeof(float4) * (size_t)r->W * r->H;
+    return RT_OK;
+}
+
+static int acc_tiles(rt_renderer *r, const uint32_t *tiles, uint32_t n, void *buf, void *stream, int unpack) {
+    if (!r || (n && (!tiles || !buf))) return fail(RT_ERR_INVALID, "null argument");
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(r->scene->device));
+    const uint32_t tiles_x = (r->W + 7) / 8, ntiles = tiles_x * ((r->H + 7) / 8);
+    for (uint32_t i = 0; i < n; ++i)
+        if (tiles[i] >= ntiles) return fail(RT_ERR_INVALID, "tile index out of range");
+    uint32_t *d_tiles = nullptr;   // one-time operations: a private copy of the list
+    HIP_TRY(hipMalloc(&d_tiles, sizeof(uint32_t) * n));
+    hipError_t e = hipMemcpy(d_tiles, tiles, sizeof(uint32_t) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_acc_tiles, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, r->d_acc,
+                           static_cast<float4 *>(buf), d_tiles, n, tiles_x, r->W, r->H, unpack);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+    (void)hipFree(d_tiles);
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("accumulator tiles: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+int rt::accumulator_pack(rt_renderer *r, const uint32_t *tiles, uint32_t n, void *buf_dev, void *stream) {
+    return acc_tiles(r, tiles, n, buf_dev, stream, 0);
+}
+
+int rt::accumulator_unpack(rt_renderer *r, const uint32_t *tiles, uint32_t n, const void *buf_dev, void *stream) {
+    return acc_tiles(r, tiles, n, const_cast<void *>(buf_dev), stream, 1);
+}
 
 int rt::renderer_geometry(const rt_renderer *r, uint32_t *W, uint32_t *H, int *device) {
     if (!r) return fail(RT_ERR_INVALID, "null renderer");
@@ -1501,6 +1605,8 @@ int rt_renderer_destroy(rt_renderer *r) {
     if (r->d_samples) (void)hipFree(r->d_samples);
     if (r->d_order) (void)hipFree(r->d_order);
     if (r->d_cost) (void)hipFree(r->d_cost);
+    if (r->d_map) (void)hipFree(r->d_map);
+    if (r->d_where) (void)hipFree(r->d_where);
     for (auto &e : r->tev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : r->sev)
@@ -1551,7 +1657,47 @@ int rt_assemble_shards(rt_renderer *r, const uint32_t *gathered, uint32_t nshard
     rt_shard_capacity(r->W, r->H, nshards, &cap);
     uint32_t tiles_x = (r->W + 7) / 8, ntiles = tiles_x * ((r->H + 7) / 8);
     hipStream_t st = (hipStream_t)stream;
-    launch_assemble(gathered, cap, nshards, tiles_x, ntiles, r->W, r->H, rgb8, st);
+    launch_assemble(gathered, cap, nshards, nullptr, tiles_x, ntiles, r->W, r->H, rgb8, st);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+int rt_render_shard_tiles(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, const uint32_t *tiles,
+                          uint32_t ntiles, uint32_t *tiles_dev, void *stream) {
+    if (!r || (ntiles && !tiles)) return fail(RT_ERR_INVALID, "rt_render_shard_tiles: null argument");
+    return launch_render(r, cam, p, 0, 1, tiles_dev, 1, stream, tiles ? tiles : reinterpret_cast<const uint32_t *>(r), ntiles);
+}
+
+int rt_assemble_tiles(rt_renderer *r, const uint32_t *gathered, uint32_t stride_px, const uint32_t *deal_tiles,
+                      const uint32_t *deal_off, uint32_t nshards, uint32_t *rgb8, void *stream) {
+    if (!r || !gathered || !deal_tiles || !deal_off || !rgb8 || !nshards || nshards > 255)
+        return fail(RT_ERR_INVALID, "rt_assemble_tiles: bad argument");
+    HIP_TRY(hipSetDevice(r->scene->device));
+    const uint32_t tiles_x = (r->W + 7) / 8, ntiles = tiles_x * ((r->H + 7) / 8);
+    if (deal_off[0] != 0 || deal_off[nshards] != ntiles) return fail(RT_ERR_INVALID, "rt_assemble_tiles: the deal must cover every tile once");
+    uint64_t h = fnv1a(deal_off, sizeof(uint32_t) * (nshards + 1u), fnv1a(deal_tiles, sizeof(uint32_t) * ntiles));
+    if (!r->d_where || h != r->where_hash) {
+        std::vector<uint32_t> where(ntiles, 0xffffffffu);
+        for (uint32_t k = 0; k < nshards; ++k) {
+            if (deal_off[k + 1] < deal_off[k] || (size_t)(deal_off[k + 1] - deal_off[k]) * 64u > stride_px)
+                return fail(RT_ERR_INVALID, "rt_assemble_tiles: a shard's tiles exceed the stride");
+            for (uint32_t i = deal_off[k]; i < deal_off[k + 1]; ++i) {
+                const uint32_t t = deal_tiles[i];
+                if (t >= ntiles || where[t] != 0xffffffffu) return fail(RT_ERR_INVALID, "rt_assemble_tiles: tile out of range or repeated");
+                where[t] = (k << 24) | (i - deal_off[k]);
+            }
+        }
+        HIP_TRY(hipDeviceSynchronize());   // an assembly may still read the previous map
+        if (!r->d_where || r->where_cap < ntiles) {
+            if (r->d_where) HIP_TRY(hipFree(r->d_where));
+            r->d_where = nullptr;
+            HIP_TRY(hipMalloc(&r->d_where, sizeof(uint32_t) * ntiles));
+            r->where_cap = ntiles;
+        }
+        HIP_TRY(hipMemcpy(r->d_where, where.data(), sizeof(uint32_t) * ntiles, hipMemcpyHostToDevice));
+        r->where_hash = h;
+    }
+    launch_assemble(gathered, stride_px, nshards, r->d_where, tiles_x, ntiles, r->W, r->H, rgb8, (hipStream_t)stream);
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }

@@ -45,6 +45,13 @@ int build_sbvh(const rt_prim *prims, const float *transforms, uint32_t n, Bvh &o
 
 // frame size and device of a renderer (rt_multi.cpp)
 int renderer_geometry(const rt_renderer *r, uint32_t *W, uint32_t *H, int *device);
+// the renderer's device accumulator (W*H float4 = 16 B each); and the accumulator values of
+// the listed 8x8 tiles packed as [i][64] float4 into buf_dev / written back from it (pixels
+// outside the frame: 0 / skipped), on `stream` -- rt_multi.cpp moves a pixel's running average
+// to its new rank when a multi-GPU deal changes owners
+int renderer_accumulator(rt_renderer *r, void **acc_dev, size_t *bytes);
+int accumulator_pack(rt_renderer *r, const uint32_t *tiles, uint32_t n, void *buf_dev, void *stream);
+int accumulator_unpack(rt_renderer *r, const uint32_t *tiles, uint32_t n, const void *buf_dev, void *stream);
 
 // SURVEY.md 8(d) scenes as descriptions
 struct SceneSource {

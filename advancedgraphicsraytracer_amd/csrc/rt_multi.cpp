@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -104,22 +105,42 @@ int comm_fail(const Rccl &R, ncclResult_t e, const char *what) {
 }  // namespace
 
 // One communicator + the per-renderer exchange buffers (double-buffered for the pipelined mode).
+// A frame is rendered under a deal (which rank owns which 8x8 tiles): the interleaved deal
+// t % world == rank, or with RT_MULTI_BALANCED -- from the kDealAfter-th frame of a parameter
+// set on -- the cost-balanced compact deal of rt_tile_deal, built once per parameter set from
+// the ranks' measured tile costs (one exchange: costs to rank 0, the deal back to every rank).
+struct Deal {
+    std::vector<uint32_t> tiles, off;      // rt_tile_deal layout
+    uint32_t count(int k) const { return off[k + 1] - off[k]; }
+};
+
 struct rt_comm {
     ncclComm_t comm = nullptr;
     bool owned = false;
     int rank = 0, world = 1, device = 0;
     hipStream_t comm_stream = nullptr;     // pipelined gathers run here, beside the next render
+    hipStream_t setup_stream = nullptr;    // the one-time deal exchange
     const rt_renderer *renderer = nullptr; // buffers below belong to this renderer's frame size
-    uint32_t cap = 0;                      // packed pixels per shard
+    uint32_t W = 0, H = 0, ntiles = 0;
+    uint32_t stride = 0;                   // packed pixels per shard slot (room for any deal)
     uint32_t *tiles[2] = {nullptr, nullptr};      // this rank's packed tiles (rank 0: unused)
-    uint32_t *gathered[2] = {nullptr, nullptr};   // rank 0: world x cap, slot 0 rendered in place
+    uint32_t *gathered[2] = {nullptr, nullptr};   // rank 0: world x stride, slot 0 rendered in place
     hipEvent_t ev_render[2] = {nullptr, nullptr}, ev_gather[2] = {nullptr, nullptr};
     hipEvent_t ev_asm[2] = {nullptr, nullptr};   // rank 0, pipelined: frame assembled (comm stream)
     hipEvent_t ev_caller = nullptr;        // rank 0, pipelined: the caller's stream at the call, so the
                                            // unshuffle into rgb8_dev follows the caller's reads of it
     int slot = 0;
     int pending = -1;                      // slot whose gather is in flight (pipelined mode)
+    int slot_deal[2] = {0, 0};             // the deal a slot's frame was rendered under: 0 interleaved, 1 balanced
     uint64_t frames = 0;
+    Deal interleaved, balanced;
+    Deal last_balanced;                    // the balanced deal the last balanced frame used
+    int last_deal = -1;                    // deal of the previous frame (-1 none yet)
+    uint64_t deal_version = 0, last_version = 0;   // balanced deals built / the one last used
+    uint64_t deal_key = 0;                 // parameter set the balanced deal belongs to
+    uint32_t key_calls = 0;                // frames of that parameter set so far
+    bool deal_on = false;
+    uint32_t *d_setup = nullptr;           // staging of the exchange
     // RT_MULTI_TIMING: per frame (render start, render end, gather end) events, summed by rt_comm_timing
     std::vector<std::array<hipEvent_t, 3>> tev;
     size_t tev_used = 0;
@@ -127,15 +148,25 @@ struct rt_comm {
 
 namespace {
 
+// frames of a parameter set rendered under the interleaved deal before the balanced one is built:
+// the renderer records its tile costs and sorts them within its first four frames
+constexpr uint32_t kDealAfter = 6;
+
 void free_buffers(rt_comm *c) {
     for (int k = 0; k < 2; ++k) {
         if (c->tiles[k]) (void)hipFree(c->tiles[k]);
         if (c->gathered[k]) (void)hipFree(c->gathered[k]);
         c->tiles[k] = c->gathered[k] = nullptr;
     }
+    if (c->d_setup) (void)hipFree(c->d_setup);
+    c->d_setup = nullptr;
     c->renderer = nullptr;
-    c->cap = 0;
+    c->stride = 0;
     c->pending = -1;
+    c->deal_on = false;
+    c->deal_key = 0;
+    c->key_calls = 0;
+    c->last_deal = -1;
 }
 
 int bind_renderer(rt_comm *c, rt_renderer *r) {
@@ -144,37 +175,49 @@ int bind_renderer(rt_comm *c, rt_renderer *r) {
     int rc = renderer_geometry(r, &W, &H, &dev);
     if (rc != RT_OK) return rc;
     if (dev != c->device) return fail(RT_ERR_INVALID, "renderer and communicator are on different devices");
-    uint32_t cap = 0;
-    rc = rt_shard_capacity(W, H, (uint32_t)c->world, &cap);
-    if (rc != RT_OK) return rc;
-    if (c->renderer == r && c->cap == cap) return RT_OK;
+    if (c->renderer == r && c->W == W && c->H == H) return RT_OK;
     if (c->pending >= 0) return fail(RT_ERR_INVALID, "rt_render_frame_multi: flush the pipelined frame before switching renderers");
     free_buffers(c);
+    const uint32_t ntiles = ((W + 7) / 8) * ((H + 7) / 8);
+    // every deal fits: a shard holds at most all tiles (a balanced deal's region may hold many cheap ones)
+    const uint32_t stride = ntiles * 64u;
     for (int k = 0; k < 2; ++k) {
-        if (c->rank == 0) HIP_TRY(hipMalloc(&c->gathered[k], sizeof(uint32_t) * (size_t)cap * c->world));
-        else HIP_TRY(hipMalloc(&c->tiles[k], sizeof(uint32_t) * (size_t)cap));
+        if (c->rank == 0) HIP_TRY(hipMalloc(&c->gathered[k], sizeof(uint32_t) * (size_t)stride * c->world));
+        else HIP_TRY(hipMalloc(&c->tiles[k], sizeof(uint32_t) * (size_t)stride));
+    }
+    HIP_TRY(hipMalloc(&c->d_setup, sizeof(uint32_t) * ((size_t)ntiles + c->world + 1)));
+    Deal &d = c->interleaved;   // t % world == rank, in tile order (rt_render_shard's packing)
+    d.tiles.clear();
+    d.off.assign(1, 0);
+    for (int k = 0; k < c->world; ++k) {
+        for (uint32_t t = (uint32_t)k; t < ntiles; t += (uint32_t)c->world) d.tiles.push_back(t);
+        d.off.push_back((uint32_t)d.tiles.size());
     }
     c->renderer = r;
-    c->cap = cap;
+    c->W = W;
+    c->H = H;
+    c->ntiles = ntiles;
+    c->stride = stride;
     c->slot = 0;
     return RT_OK;
 }
 
 // the frame's one collective: every rank's packed tiles to rank 0 (rank 0's own shard was
-// rendered in place into slot 0 of the gather buffer)
-int gather(rt_comm *c, int k, hipStream_t st) {
+// rendered in place into slot 0 of the gather buffer); each peer sends its deal's tile count
+int gather(rt_comm *c, int k, const Deal &d, hipStream_t st) {
     const Rccl &R = rccl();
-    const size_t bytes = sizeof(uint32_t) * (size_t)c->cap;
     NCCL_TRY(R, R.group_start(), "ncclGroupStart");
     if (c->rank == 0) {
         for (int peer = 1; peer < c->world; ++peer) {
-            ncclResult_t e = R.recv(c->gathered[k] + (size_t)peer * c->cap, bytes, ncclUint8, peer, c->comm, st);
+            const size_t bytes = sizeof(uint32_t) * 64u * d.count(peer);
+            ncclResult_t e = R.recv(c->gathered[k] + (size_t)peer * c->stride, bytes, ncclUint8, peer, c->comm, st);
             if (e != ncclSuccess) {
                 (void)R.group_end();
                 return comm_fail(R, e, "ncclRecv");
             }
         }
     } else {
+        const size_t bytes = sizeof(uint32_t) * 64u * d.count(c->rank);
         ncclResult_t e = R.send(c->tiles[k], bytes, ncclUint8, 0, c->comm, st);
         if (e != ncclSuccess) {
             (void)R.group_end();
@@ -197,12 +240,183 @@ unsigned sync_event_flags() {
 int assemble(rt_comm *c, rt_renderer *r, int k, uint32_t *rgb8, hipStream_t st) {
     if (c->rank != 0) return RT_OK;
     if (!rgb8) return fail(RT_ERR_INVALID, "rt_render_frame_multi: rank 0 needs an output frame");
-    return rt_assemble_shards(r, c->gathered[k], (uint32_t)c->world, rgb8, st);
+    const Deal &d = c->slot_deal[k] ? c->balanced : c->interleaved;
+    return rt_assemble_tiles(r, c->gathered[k], c->stride, d.tiles.data(), d.off.data(), (uint32_t)c->world, rgb8, st);
+}
+
+uint64_t params_key(const rt_camera *cam, const rt_frame_params *p) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void *d, size_t n) {
+        const unsigned char *q = static_cast<const unsigned char *>(d);
+        for (size_t i = 0; i < n; ++i) h = (h ^ q[i]) * 1099511628211ull;
+    };
+    mix(cam, sizeof(*cam));
+    mix(&p->width, sizeof(uint32_t) * 4);   // width height spp depth
+    mix(&p->mode, sizeof(uint32_t));
+    return h;
+}
+
+// The one-time exchange behind the balanced deal (every rank, the same call): each rank's
+// measured costs of its interleaved tiles to rank 0, rank 0 builds rt_tile_deal over the whole
+// frame (equal costs when any rank has none, e.g. path-traced frames), the deal back to every
+// rank.  Blocking: it runs once per parameter set.
+int exchange_deal(rt_comm *c, rt_renderer *r) {
+    const Rccl &R = rccl();
+    if (!c->setup_stream) HIP_TRY(hipStreamCreateWithFlags(&c->setup_stream, hipStreamNonBlocking));
+    const Deal &il = c->interleaved;
+    const uint32_t mine = il.count(c->rank);
+    std::vector<uint32_t> cost(mine, 0u);
+    uint32_t have = 0;
+    int rc = rt_renderer_tile_costs(r, cost.data(), mine, &have);
+    if (rc != RT_OK) return rc;
+    if (have != mine) std::fill(cost.begin(), cost.end(), 0u);   // none recorded: 0 = "no costs"
+    hipStream_t st = c->setup_stream;
+    std::vector<uint32_t> all(c->ntiles, 0u);
+    if (c->rank == 0) {
+        std::copy(cost.begin(), cost.end(), all.begin());
+        if (c->world > 1) {
+            NCCL_TRY(R, R.group_start(), "ncclGroupStart");
+            for (int peer = 1; peer < c->world; ++peer)
+                NCCL_TRY(R, R.recv(c->d_setup + il.off[peer], sizeof(uint32_t) * il.count(peer), ncclUint8, peer, c->comm, st), "ncclRecv");
+            NCCL_TRY(R, R.group_end(), "ncclGroupEnd");
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipMemcpy(all.data() + il.off[1], c->d_setup + il.off[1], sizeof(uint32_t) * (c->ntiles - il.off[1]),
+                              hipMemcpyDeviceToHost));
+        }
+        // local order -> global tile; a rank without costs (zeros) makes the deal count-balanced
+        std::vector<uint32_t> global(c->ntiles, 0u);
+        bool complete = true;
+        for (int k = 0; k < c->world; ++k) {
+            bool any = false;
+            for (uint32_t i = il.off[k]; i < il.off[k + 1]; ++i) {
+                global[il.tiles[i]] = all[i];
+                any = any || all[i] != 0;
+            }
+            complete = complete && (any || il.count(k) == 0);
+        }
+        Deal &d = c->balanced;
+        d.tiles.assign(c->ntiles, 0u);
+        d.off.assign((size_t)c->world + 1, 0u);
+        if ((rc = rt_tile_deal(c->W, c->H, complete ? global.data() : nullptr, (uint32_t)c->world, d.tiles.data(),
+                               d.off.data())) != RT_OK)
+            return rc;
+        if (c->world > 1) {
+            std::vector<uint32_t> msg(d.off);
+            msg.insert(msg.end(), d.tiles.begin(), d.tiles.end());
+            HIP_TRY(hipMemcpy(c->d_setup, msg.data(), sizeof(uint32_t) * msg.size(), hipMemcpyHostToDevice));
+            NCCL_TRY(R, R.group_start(), "ncclGroupStart");
+            for (int peer = 1; peer < c->world; ++peer)
+                NCCL_TRY(R, R.send(c->d_setup, sizeof(uint32_t) * msg.size(), ncclUint8, peer, c->comm, st), "ncclSend");
+            NCCL_TRY(R, R.group_end(), "ncclGroupEnd");
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+    } else {
+        HIP_TRY(hipMemcpy(c->d_setup, cost.data(), sizeof(uint32_t) * mine, hipMemcpyHostToDevice));
+        NCCL_TRY(R, R.send(c->d_setup, sizeof(uint32_t) * mine, ncclUint8, 0, c->comm, st), "ncclSend");
+        HIP_TRY(hipStreamSynchronize(st));
+        const size_t words = (size_t)c->world + 1 + c->ntiles;
+        NCCL_TRY(R, R.recv(c->d_setup, sizeof(uint32_t) * words, ncclUint8, 0, c->comm, st), "ncclRecv");
+        HIP_TRY(hipStreamSynchronize(st));
+        std::vector<uint32_t> msg(words);
+        HIP_TRY(hipMemcpy(msg.data(), c->d_setup, sizeof(uint32_t) * words, hipMemcpyDeviceToHost));
+        c->balanced.off.assign(msg.begin(), msg.begin() + c->world + 1);
+        c->balanced.tiles.assign(msg.begin() + c->world + 1, msg.end());
+    }
+    c->deal_on = true;
+    c->deal_version += 1;
+    return RT_OK;
+}
+
+// Tiles change owner between two frames (interleaved <-> balanced deal): a pixel's running
+// average (renderer.cpp:235-241) must go on from the frames its previous owner accumulated.
+// Every rank packs its accumulator values of the tiles it owned under the old deal, rank 0
+// writes them into its accumulator (now the whole frame's) and hands that to every rank.
+// Collective and blocking; once per deal switch.
+int migrate_accumulators(rt_comm *c, rt_renderer *r, const Deal &old) {
+    const Rccl &R = rccl();
+    if (!c->setup_stream) HIP_TRY(hipStreamCreateWithFlags(&c->setup_stream, hipStreamNonBlocking));
+    hipStream_t st = c->setup_stream;
+    HIP_TRY(hipDeviceSynchronize());   // every frame so far has updated its accumulator
+    void *acc = nullptr;
+    size_t bytes = 0;
+    int rc = renderer_accumulator(r, &acc, &bytes);
+    if (rc != RT_OK) return rc;
+    uint32_t most = 0;
+    for (int k = 0; k < c->world; ++k) most = std::max(most, old.count(k));
+    void *staging = nullptr;
+    HIP_TRY(hipMalloc(&staging, std::max<size_t>(16, (size_t)most * 64u * 16u)));
+    auto run = [&]() -> int {
+        if (c->rank == 0) {
+            for (int peer = 1; peer < c->world; ++peer) {
+                const uint32_t n = old.count(peer);
+                if (!n) continue;
+                NCCL_TRY(R, R.recv(staging, (size_t)n * 64u * 16u, ncclUint8, peer, c->comm, st), "ncclRecv");
+                HIP_TRY(hipStreamSynchronize(st));
+                int e = accumulator_unpack(r, old.tiles.data() + old.off[peer], n, staging, st);
+                if (e != RT_OK) return e;
+            }
+            NCCL_TRY(R, R.group_start(), "ncclGroupStart");
+            for (int peer = 1; peer < c->world; ++peer)
+                NCCL_TRY(R, R.send(acc, bytes, ncclUint8, peer, c->comm, st), "ncclSend");
+            NCCL_TRY(R, R.group_end(), "ncclGroupEnd");
+            HIP_TRY(hipStreamSynchronize(st));
+        } else {
+            const uint32_t n = old.count(c->rank);
+            if (n) {
+                int e = accumulator_pack(r, old.tiles.data() + old.off[c->rank], n, staging, st);
+                if (e != RT_OK) return e;
+                NCCL_TRY(R, R.send(staging, (size_t)n * 64u * 16u, ncclUint8, 0, c->comm, st), "ncclSend");
+                HIP_TRY(hipStreamSynchronize(st));
+            }
+            NCCL_TRY(R, R.recv(acc, bytes, ncclUint8, 0, c->comm, st), "ncclRecv");
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+        return RT_OK;
+    };
+    rc = run();
+    (void)hipFree(staging);
+    return rc;
 }
 
 }  // namespace
 
 extern "C" {
+
+// Cost-balanced, spatially compact tile deal: the frame's 8x8 tiles in Morton (Z) order of
+// their (x, y), cut into nshards runs of equal summed cost (cost == NULL: one per tile).  A
+// rank then renders one compact screen region -- its GPU's caches hold the nodes of that
+// region only -- whose measured cost is 1/nshards of the frame's, where the interleaved deal
+// (t % nshards) spreads every rank over the whole screen.
+int rt_tile_deal(uint32_t width, uint32_t height, const uint32_t *cost, uint32_t nshards, uint32_t *deal_tiles,
+                 uint32_t *deal_off) {
+    if (!width || !height || !nshards || nshards > 255 || !deal_tiles || !deal_off)
+        return fail(RT_ERR_INVALID, "rt_tile_deal: bad argument");
+    const uint32_t tx = (width + 7) / 8, ty = (height + 7) / 8, n = tx * ty;
+    auto morton = [](uint32_t x, uint32_t y) {
+        uint64_t m = 0;
+        for (int b = 0; b < 16; ++b) m |= (uint64_t)((x >> b) & 1u) << (2 * b) | (uint64_t)((y >> b) & 1u) << (2 * b + 1);
+        return m;
+    };
+    std::vector<uint64_t> key(n);
+    for (uint32_t t = 0; t < n; ++t) {
+        key[t] = morton(t % tx, t / tx);
+        deal_tiles[t] = t;
+    }
+    std::sort(deal_tiles, deal_tiles + n, [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+    std::vector<double> prefix(n + 1, 0.0);
+    for (uint32_t i = 0; i < n; ++i) prefix[i + 1] = prefix[i] + (cost ? (double)cost[deal_tiles[i]] : 1.0);
+    const double total = prefix[n];
+    deal_off[0] = 0;
+    for (uint32_t k = 1; k < nshards; ++k) {
+        // first index whose prefix reaches k / nshards of the cost (ties: the nearer boundary)
+        const double target = total * k / nshards;
+        uint32_t b = (uint32_t)(std::lower_bound(prefix.begin(), prefix.end(), target) - prefix.begin());
+        if (b > 0 && b <= n && target - prefix[b - 1] < prefix[b] - target) --b;
+        deal_off[k] = std::min(n, std::max(b, deal_off[k - 1]));
+    }
+    deal_off[nshards] = n;
+    return RT_OK;
+}
 
 int rt_comm_unique_id(uint8_t *id) {
     if (!id) return fail(RT_ERR_INVALID, "rt_comm_unique_id: null argument");
@@ -278,6 +492,7 @@ int rt_comm_destroy(rt_comm *c) {
     for (auto &e : c->tev)
         for (auto &x : e) (void)hipEventDestroy(x);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+    if (c->setup_stream) (void)hipStreamDestroy(c->setup_stream);
     if (c->owned && c->comm) (void)rccl().comm_destroy(c->comm);
     delete c;
     return RT_OK;
@@ -286,7 +501,8 @@ int rt_comm_destroy(rt_comm *c) {
 int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, const rt_frame_params *p,
                           uint32_t *rgb8_dev, uint32_t flags, void *stream) {
     if (!r || !c || !cam || !p) return fail(RT_ERR_INVALID, "rt_render_frame_multi: null argument");
-    if (flags & ~(uint32_t)(RT_MULTI_PIPELINED | RT_MULTI_TIMING)) return fail(RT_ERR_INVALID, "rt_render_frame_multi: unknown flags");
+    if (flags & ~(uint32_t)(RT_MULTI_PIPELINED | RT_MULTI_TIMING | RT_MULTI_BALANCED))
+        return fail(RT_ERR_INVALID, "rt_render_frame_multi: unknown flags");
     const bool pipelined = (flags & RT_MULTI_PIPELINED) != 0;
     // every check before the first side effect: a rejected call leaves the accumulator, the
     // frame count and the communicator as they were
@@ -312,7 +528,30 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
     // or display of the frame before) must be done with rgb8_dev first
     const bool assemble_prev = pipelined && c->rank == 0 && c->pending >= 0;
     if (assemble_prev) HIP_TRY(hipEventRecord(c->ev_caller, st));
+    // the deal of this frame: interleaved, or (RT_MULTI_BALANCED) the balanced deal of this
+    // parameter set, exchanged once on its kDealAfter-th frame
+    const uint64_t key = params_key(cam, p);
+    if (key != c->deal_key) {
+        c->deal_key = key;
+        c->key_calls = 0;
+        c->deal_on = false;
+    }
+    if ((flags & RT_MULTI_BALANCED) && !c->deal_on && c->key_calls >= kDealAfter && (rc = exchange_deal(c, r)) != RT_OK)
+        return rc;
+    c->key_calls += 1;
+    const bool use_balanced = (flags & RT_MULTI_BALANCED) && c->deal_on;
+    const Deal &deal = use_balanced ? c->balanced : c->interleaved;
+    const int deal_id = use_balanced ? 1 : 0;
+    if (c->world > 1 && c->last_deal >= 0 && (c->last_deal != deal_id || (deal_id == 1 && c->last_version != c->deal_version))) {
+        // the frames before were rendered under another deal: move the accumulators first
+        // (pending pipelined work is finished by the device-wide sync inside)
+        if ((rc = migrate_accumulators(c, r, c->last_deal == 1 ? c->last_balanced : c->interleaved)) != RT_OK) return rc;
+    }
+    if (deal_id == 1 && c->last_version != c->deal_version) c->last_balanced = c->balanced;
+    c->last_deal = deal_id;
+    c->last_version = c->deal_version;
     const int k = c->slot;
+    c->slot_deal[k] = deal_id;
     uint32_t *mine = c->rank == 0 ? c->gathered[k] : c->tiles[k];
     std::array<hipEvent_t, 3> *tv = nullptr;
     if (flags & RT_MULTI_TIMING) {
@@ -324,11 +563,14 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
         tv = &c->tev[c->tev_used++];
         HIP_TRY(hipEventRecord((*tv)[0], st));
     }
-    rc = rt_render_shard(r, cam, p, (uint32_t)c->rank, (uint32_t)c->world, mine, st);
+    if (use_balanced)
+        rc = rt_render_shard_tiles(r, cam, p, deal.tiles.data() + deal.off[c->rank], deal.count(c->rank), mine, st);
+    else
+        rc = rt_render_shard(r, cam, p, (uint32_t)c->rank, (uint32_t)c->world, mine, st);
     if (rc != RT_OK) return rc;
     if (tv) HIP_TRY(hipEventRecord((*tv)[1], st));
     if (!pipelined) {
-        if ((rc = gather(c, k, st)) != RT_OK) return rc;   // in stream order after the render
+        if ((rc = gather(c, k, deal, st)) != RT_OK) return rc;   // in stream order after the render
         if (tv) HIP_TRY(hipEventRecord((*tv)[2], st));
         if ((rc = assemble(c, r, k, rgb8_dev, st)) != RT_OK) return rc;
         c->frames += 1;
@@ -355,7 +597,7 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
     }
     HIP_TRY(hipEventRecord(c->ev_render[k], st));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_render[k], 0));
-    if ((rc = gather(c, k, c->comm_stream)) != RT_OK) return rc;
+    if ((rc = gather(c, k, deal, c->comm_stream)) != RT_OK) return rc;
     HIP_TRY(hipEventRecord(c->ev_gather[k], c->comm_stream));
     if (tv) HIP_TRY(hipEventRecord((*tv)[2], c->comm_stream));
     c->pending = k;

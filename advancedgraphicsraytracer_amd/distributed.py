@@ -141,8 +141,8 @@ class NativeShardedFrame:
     runs the frame's RCCL gather from C++ (rt_multi.cpp); rank 0 assembles.  Same interface
     as ShardedFrame.  The process group (any backend) carries only the RCCL unique id."""
 
-    def __init__(self, renderer, group=None, device=None, timing=False):
-        from . import RT_COMM_ID_BYTES, MULTI_PIPELINED, MULTI_TIMING, _check, lib
+    def __init__(self, renderer, group=None, device=None, timing=False, balanced=False):
+        from . import RT_COMM_ID_BYTES, MULTI_BALANCED, MULTI_PIPELINED, MULTI_TIMING, _check, lib
         self.L, self._check = lib(), _check
         self.r = renderer
         self.world = dist.get_world_size(group)
@@ -158,6 +158,8 @@ class NativeShardedFrame:
         _check(self.L.rt_comm_create(uid, self.rank, self.world, self.device.index or 0, C.byref(self.h)))
         self.frame = torch.zeros(renderer.width * renderer.height, dtype=torch.int32, device=self.device)
         self._pipelined, self._timing_flag = MULTI_PIPELINED, (MULTI_TIMING if timing else 0)
+        # RT_MULTI_BALANCED: the cost-balanced compact tile deal from a parameter set's 7th frame on
+        self._deal_flag = MULTI_BALANCED if balanced else 0
         self._pending = False
 
     def _stream(self, stream):
@@ -167,7 +169,8 @@ class NativeShardedFrame:
         p = self.r.params(spp, depth, frame)
         out = C.c_void_p(self.frame.data_ptr()) if self.rank == 0 else None
         self._check(self.L.rt_render_frame_multi(self.r.h, self.h, C.byref(self.r.camera), C.byref(p), out,
-                                                 flags | self._timing_flag, C.c_void_p(self._stream(stream))))
+                                                 flags | self._timing_flag | self._deal_flag,
+                                                 C.c_void_p(self._stream(stream))))
 
     def render(self, spp=1, depth=10, frame=0, stream=None):
         """One frame, in stream order: render, gather, rank-0 assembly.  The frame on rank 0."""

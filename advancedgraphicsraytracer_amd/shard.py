@@ -43,3 +43,48 @@ def assemble_host(gathered, width, height, world):
         ok = px >= 0
         frame[px[ok]] = gathered[s][ok]
     return frame
+
+
+# ---- explicit deals (rt_tile_deal / rt_render_shard_tiles / rt_assemble_tiles)
+def _morton(x, y):
+    m = np.zeros_like(x, dtype=np.uint64)
+    for b in range(16):
+        m |= ((x >> b) & 1).astype(np.uint64) << np.uint64(2 * b)
+        m |= ((y >> b) & 1).astype(np.uint64) << np.uint64(2 * b + 1)
+    return m
+
+
+def tile_deal_host(width, height, num_shards, cost=None):
+    """Host mirror of rt_tile_deal: the tiles in Morton order of (tx, ty), cut into num_shards
+    runs of equal summed cost (boundary at the prefix nearest to k/num_shards of the total)."""
+    tx, ty = tile_grid(width, height)
+    n = tx * ty
+    t = np.arange(n)
+    tiles = t[np.argsort(_morton(t % tx, t // tx), kind="stable")].astype(np.uint32)
+    c = np.ones(n) if cost is None else np.asarray(cost, np.float64)[tiles]
+    prefix = np.concatenate([[0.0], np.cumsum(c)])
+    total = prefix[-1]
+    off = [0]
+    for k in range(1, num_shards):
+        target = total * k / num_shards
+        b = int(np.searchsorted(prefix, target, side="left"))
+        if 0 < b <= n and target - prefix[b - 1] < prefix[b] - target:
+            b -= 1
+        off.append(min(n, max(b, off[-1])))
+    off.append(n)
+    return tiles, np.asarray(off, np.uint32)
+
+
+def assemble_host_deal(gathered, width, height, stride, deal_tiles, deal_off):
+    """gathered: [num_shards * stride] packed shards of an explicit deal -> [H*W] frame."""
+    tx, _ = tile_grid(width, height)
+    frame = np.zeros(width * height, np.asarray(gathered).dtype)
+    g = np.asarray(gathered).reshape(-1)
+    lane = np.arange(TILE * TILE)
+    for k in range(len(deal_off) - 1):
+        for i, t in enumerate(deal_tiles[deal_off[k]:deal_off[k + 1]]):
+            x = (t % tx) * TILE + (lane & 7)
+            y = (t // tx) * TILE + (lane >> 3)
+            ok = (x < width) & (y < height)
+            frame[(x + y * width)[ok]] = g[k * stride + i * 64 + lane[ok]]
+    return frame

@@ -47,8 +47,16 @@ def _path_traced(argv):
 # share a queue with the caller's (world-1 multi frame, mig29 x16: 0.471 -> 0.327 ms; TEAPOT-F
 # 0.128 either way; profiles/r02/multi_overhead_hwq8.log).  Single-GPU primary+shadow runs keep
 # HIP's default.  Set before HIP initialises.
-if _path_traced(sys.argv[1:]) or int(os.environ.get("WORLD_SIZE", "1")) > 1:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# The box may export its own value (HIP's default is 4): the bench sets 8 explicitly where its
+# design needs it and records the value in effect (config.hip_hw_queues).  --hw-queues N
+# overrides; never above 32 (the pool refuses more).
+_HWQ_BEFORE = os.environ.get("GPU_MAX_HW_QUEUES")
+_HWQ_ARG = next((a.partition("=")[2] or (sys.argv[i + 2] if i + 2 < len(sys.argv) else "")
+                 for i, a in enumerate(sys.argv[1:]) if a.startswith("--hw-queues")), None)
+if _HWQ_ARG:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, int(_HWQ_ARG))))
+elif _path_traced(sys.argv[1:]) or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -97,6 +105,8 @@ def parse():
     ap.add_argument("--per-step-events", action="store_true", help="HIP event pair around every launch at N = 1 too")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the all-cores CPU baseline sample")
     ap.add_argument("--summary", default=rl.SUMMARY, help="rocprofv3 PMC / kernel-trace summary (tools/roofline.py)")
+    ap.add_argument("--hw-queues", type=int, default=None, help="GPU_MAX_HW_QUEUES for this run (applied before HIP "
+                    "starts; default: 8 for path-traced and N > 1 runs, else the environment's / HIP's default)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     args.scene = args.scene or cfg["scene"]
@@ -366,7 +376,10 @@ def main():
                                    + (" (primary + NEE shadow)" if args.depth == 1 else " (path tracing)")
                                    + ", accumulate + RGB8",
                        "scene": args.scene, "width": W, "height": H, "spp": spp, "depth": args.depth,
-                       "parallelism": f"screen-tile x{world}" if world > 1 else "single GPU"},
+                       "parallelism": f"screen-tile x{world}" if world > 1 else "single GPU",
+                       "hip_hw_queues": {"effective": os.environ.get("GPU_MAX_HW_QUEUES", "4 (HIP default)"),
+                                         "set_by_bench": os.environ.get("GPU_MAX_HW_QUEUES") != _HWQ_BEFORE
+                                         or _HWQ_ARG is not None, "environment_before": _HWQ_BEFORE}},
             "fps": round(args.steps / wall, 3),
             "msamples_per_s": round(W * H * spp / (wall / args.steps) / 1e6, 3),
             "rays": {"primary": int(tot_primary), "shadow": int(tot_shadow), "bounce": int(tot_bounce),

@@ -247,6 +247,21 @@ int rt_render_shard(rt_renderer *r, const rt_camera *cam, const rt_frame_params 
  * buffers (each rt_shard_capacity pixels) -> rgb8_dev[W*H]. */
 int rt_assemble_shards(rt_renderer *r, const uint32_t *gathered_dev, uint32_t num_shards, uint32_t *rgb8_dev,
                        void *stream);
+/* Explicit tile deals (cost-balanced multi-GPU frames).  A deal lists every 8x8 tile of the
+ * frame (row-major tile index t = ty * ceil(W/8) + tx) once: shard k owns
+ * deal_tiles[deal_off[k] .. deal_off[k+1]).
+ * rt_tile_deal: the Morton-ordered tiles cut into num_shards runs of equal summed cost
+ *   (cost[t] per tile, e.g. rt_renderer_tile_costs of a full frame; NULL = equal costs):
+ *   deal_tiles[ceil(W/8) * ceil(H/8)], deal_off[num_shards + 1].
+ * rt_render_shard_tiles: the listed tiles (in that order) of one frame, packed as [i][64]
+ *   into tiles_dev -- Renderer::Tick's pixel loop over those tiles only.
+ * rt_assemble_tiles: rank 0's unshuffle; shard k's packed tiles at gathered_dev + k * stride_px. */
+int rt_tile_deal(uint32_t width, uint32_t height, const uint32_t *cost, uint32_t num_shards, uint32_t *deal_tiles,
+                 uint32_t *deal_off);
+int rt_render_shard_tiles(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, const uint32_t *tiles,
+                          uint32_t num_tiles, uint32_t *tiles_dev, void *stream);
+int rt_assemble_tiles(rt_renderer *r, const uint32_t *gathered_dev, uint32_t stride_px, const uint32_t *deal_tiles,
+                      const uint32_t *deal_off, uint32_t num_shards, uint32_t *rgb8_dev, void *stream);
 /* ---- multi-GPU frames (one process per GPU) ---------------
  * Replaces the OpenMP pixel loop of Renderer::Tick (renderer.cpp:213-245) across the GPUs of
  * a node: rank k renders the 8x8 tiles t with t % world == k, then ONE RCCL gather per frame
@@ -271,6 +286,12 @@ int rt_comm_destroy(rt_comm *c);
 #define RT_MULTI_PIPELINED 1u
 /* RT_MULTI_TIMING: HIP events around this rank's render and its gather, summed by rt_comm_timing */
 #define RT_MULTI_TIMING 2u
+/* RT_MULTI_BALANCED: from the 7th frame of a parameter set (camera, size, spp, depth, mode) on,
+ * the ranks render the cost-balanced compact deal of rt_tile_deal instead of t % world: built
+ * once per parameter set from every rank's measured tile costs (rt_renderer_tile_costs; equal
+ * costs where none were measured) in one exchange -- the costs to rank 0, the deal back to all.
+ * Frames are identical under any deal; every rank must pass the same flags. */
+#define RT_MULTI_BALANCED 4u
 int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, const rt_frame_params *p,
                           uint32_t *rgb8_dev, uint32_t flags, void *stream);
 int rt_multi_flush(rt_renderer *r, rt_comm *c, uint32_t *rgb8_dev, void *stream);

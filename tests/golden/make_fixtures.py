@@ -73,10 +73,16 @@ def main():
         pt[f"{recipe}_spp{spp}_d{depth}_pixels"] = px
         pt[f"{recipe}_spp{spp}_d{depth}_rgb"] = rgb
     np.savez_compressed(os.path.join(HERE, "pt_subsets.npz"), **pt)
+    geometry_digests()
+
+
+def geometry_digests():
     # 5. geometry digests: the recipes' primitive records after the OBJ
-    #    load (library) and the plain BVH (nodes with the unused slot 1 zeroed + indices, oracle)
+    #    load (library) and the plain BVH (nodes with the unused slot 1 zeroed + indices, oracle);
+    #    "default" = the reference's as-shipped Scene() (template/scene.h:40-128)
+    import advancedgraphicsraytracer_amd as rt
     geo = {}
-    for recipe in ("teapotF", "cfg3", "cfg5", "mig16"):
+    for recipe in ("teapotF", "cfg3", "cfg5", "mig16", "default"):
         prims, _ = rt.recipe_describe(recipe)
         sc = pyoracle.Scene(recipe, DATA_DIR)
         nodes = sc.nodes().copy()
@@ -104,4 +110,7 @@ def bvh_digest(nodes, indices):
 
 
 if __name__ == "__main__":
-    main()
+    if "--geometry-only" in sys.argv:
+        geometry_digests()
+    else:
+        main()

@@ -149,7 +149,7 @@ def parse_pt(key):
     return recipe, int(spp[3:]), int(depth[1:])
 
 
-@pytest.mark.parametrize("recipe", ["teapotF", "cfg3", "cfg5", "mig16"])
+@pytest.mark.parametrize("recipe", ["teapotF", "cfg3", "cfg5", "mig16", "default"])
 def test_geometry_digests(rt, oracle, recipe):
     """The recipe's primitive records after the OBJ load, and the plain BVH (library host build
     and oracle) hash to the committed digests."""

@@ -31,7 +31,8 @@ def test_standin_library_exports_the_rccl_subset():
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,mode,recipe,W,H", [(2, "sync", "teapotF", 200, 120), (2, "pipelined", "teapotF", 200, 120),
                                                    (3, "sync", "cfg3", 136, 80), (3, "pipelined", "mig16", 200, 120),
-                                                   (3, "pipelined", "teapotF", 16, 8)])
+                                                   (3, "pipelined", "teapotF", 16, 8), (2, "balanced", "teapotF", 200, 120),
+                                                   (3, "balanced", "mig16", 256, 144), (1, "balanced", "cfg3", 136, 80)])
 def test_multi_frame_world_n_on_one_gpu(world, mode, recipe, W, H):
     assert os.path.exists(STANDIN), "tests/cpp/libinproc_rccl.so must be built beforehand (__graft_entry__.build())"
     env = dict(os.environ, RT_RCCL_LIB=STANDIN)

@@ -22,11 +22,12 @@ for s in "$@"; do
         bench) step bench 600 python bench.py --steps 30 --warmup 5 ;;
         benchdrv) step bench_drv 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
         shard)     # per-rank frame times of the N > 1 workloads on one GPU (tools/shard_time.py)
-            step shard_mig 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --out gpurun_out/shard_time.jsonl
-            step shard_tp 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene teapotF --out gpurun_out/shard_time.jsonl ;;
+            step shard_mig 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --deal interleaved,balanced --out gpurun_out/shard_time.jsonl
+            step shard_tp 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene teapotF --deal interleaved,balanced --out gpurun_out/shard_time.jsonl ;;
         shard5)
-            step shard_cfg5 600 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 12 --frames 10 --out gpurun_out/shard_time.jsonl
-            step shard_cfg3 600 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg3 --depth 4 --spp 4 --warm 12 --frames 10 --out gpurun_out/shard_time.jsonl ;;
+            step shard_cfg5 600 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --deal interleaved,balanced --ranks last --out gpurun_out/shard_time.jsonl
+            step shard_cfg3 600 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg3 --depth 4 --spp 4 --warm 6 --frames 6 --deal interleaved,balanced --ranks last --out gpurun_out/shard_time.jsonl ;;
+        region) step region 300 python tools/timed_region.py --out gpurun_out/timed_region.jsonl ;;
         benchcfg)
             step bench_cfg3 300 python bench.py --config 3 --steps 10 --warmup 2 --no-cpu-baseline
             step bench_cfg4 300 python bench.py --config 4 --steps 30 --warmup 5 --no-cpu-baseline

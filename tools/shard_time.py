@@ -1,8 +1,13 @@
 #!/usr/bin/env python3
-"""Per-rank frame time of bench.py's N > 1 workload, measured on one GPU: the 1/N screen
-shard at spp = N (weak scaling), render + (rank-0) assembly, for N = 1, 2, 4, 8.
-Predicts the driver's scaling efficiency up to the gather.
-usage: shard_time.py [--scene teapotF] [--depth 1] [--spp S] [--strong] [--frames 30] [--out file.jsonl]
+"""Per-rank frame time of bench.py's N > 1 workload, measured on one GPU: every rank's share of
+the frame (its 1/N of the tiles) rendered back to back on a renderer of its own, for N = 1, 2,
+4, 8; the slowest rank bounds the frame.  Predicts the driver's scaling efficiency up to the
+gather.  Deals: "interleaved" (t % N, rt_render_shard) or "balanced" (rt_tile_deal over the
+measured tile costs of a full frame, rt_render_shard_tiles -- what RT_MULTI_BALANCED switches to).
+Weak scaling: spp = N x --spp per rank; --strong: one frame of --spp split N ways.
+
+usage: shard_time.py [--scene teapotF] [--depth 1] [--spp S] [--strong] [--deal interleaved,balanced]
+                     [--frames 30] [--warm 80] [--ranks all|last] [--out file.jsonl]
 (RT_SPLIT_UNITS=U: split threshold; RT_PS_PIPELINE / RT_PS_DEPTH: frames in flight)"""
 import argparse
 import json
@@ -18,6 +23,33 @@ sys.path.insert(0, ROOT)
 import advancedgraphicsraytracer_amd as rt  # noqa: E402
 
 
+def time_share(scene, a, spp, frames, render):
+    """warm-up frames (walk timing, tile order, frames-in-flight timing), then `frames` timed."""
+    r = rt.Renderer(scene, a.w, a.h)
+    st = torch.cuda.Stream()
+    for f in range(a.warm):
+        render(r, spp, f, st.cuda_stream)
+    torch.cuda.synchronize()
+    c0 = r.counters()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    with torch.cuda.stream(st):
+        ev[0].record()
+        for f in range(frames):
+            render(r, spp, a.warm + f, st.cuda_stream)
+        ev[1].record()
+    torch.cuda.synchronize()
+    c1 = r.counters()
+    ms = ev[0].elapsed_time(ev[1]) / frames
+    rays = sum(c1[k] - c0[k] for k in ("primary", "shadow", "bounce")) / frames
+    out = {"ms": round(ms, 4), "mrays": round(rays / 1e6, 3), "in_flight": r.overlap_depth()[0]}
+    cost = r.tile_costs().astype(np.float64)
+    if cost.size:
+        out["tile_cycles_max"] = int(cost.max())
+        out["tile_cycles_sum"] = int(cost.sum())
+    r.close()
+    return out, cost
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scene", default="teapotF")
@@ -30,10 +62,11 @@ def main():
     ap.add_argument("--strong", action="store_true", help="the config's spp per shard (one frame split N ways)")
     ap.add_argument("--spp", type=int, default=1, help="samples per pixel of the whole frame (strong) / per GPU (weak)")
     ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--deal", default="interleaved", help="comma list: interleaved, balanced")
+    ap.add_argument("--ranks", default="all", choices=("all", "last"), help="time every rank's share or the last only")
     ap.add_argument("--out", default=None, help="append the summary line to this jsonl file")
     a = ap.parse_args()
     scene = rt.Scene.recipe(a.scene)
-    out = {}
     r0 = rt.Renderer(scene, a.w, a.h)                  # GPU clock ramp (untimed), as bench.py
     o0 = torch.zeros(a.w * a.h, dtype=torch.int32, device="cuda")
     t0, f = time.perf_counter(), 0
@@ -44,42 +77,44 @@ def main():
             torch.cuda.synchronize()
     torch.cuda.synchronize()
     r0.close()
-    for n in [int(x) for x in a.ns.split(",")]:   # warm-up frames: walk timing, tile order, overlap timing settle first
-        r = rt.Renderer(scene, a.w, a.h)
-        cap = r.shard_capacity(n)
-        tiles = torch.zeros(cap, dtype=torch.int32, device="cuda")
-        st = torch.cuda.Stream()
-        spp = a.spp if a.strong else a.spp * n
-        for f in range(a.warm):
-            r.render_shard(tiles, n - 1, n, spp=spp, depth=a.depth, frame=f, stream=st.cuda_stream)
-        torch.cuda.synchronize()
-        c0 = r.counters()
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        with torch.cuda.stream(st):
-            ev[0].record()
-            for f in range(a.frames):
-                r.render_shard(tiles, n - 1, n, spp=spp, depth=a.depth, frame=a.warm + f, stream=st.cuda_stream)
-            ev[1].record()
-        torch.cuda.synchronize()
-        c1 = r.counters()
-        ms = ev[0].elapsed_time(ev[1]) / a.frames
-        rays = sum(c1[k] - c0[k] for k in ("primary", "shadow", "bounce")) / a.frames
-        out[n] = {"ms_per_frame": round(ms, 4), "mrays_s_per_gpu": round(rays / (ms * 1e-3) / 1e6, 1),
-                  "in_flight": r.overlap_depth()[0], "groups_ms": r.overlap_depth()[1]}
-        cost = r.tile_costs().astype(np.float64)
-        if cost.size:   # the shard's per-tile wave cycles (s_memtime ticks) behind its tile order
-            out[n]["tile_cycles"] = {"tiles": int(cost.size), "max": int(cost.max()), "p99": int(np.percentile(cost, 99)),
-                                     "mean": round(float(cost.mean()), 1), "sum": int(cost.sum())}
-        print(n, json.dumps(out[n]), flush=True)
-        r.close()
-    base = out[1]["mrays_s_per_gpu"]
-    line = json.dumps({"scene": a.scene, "depth": a.depth, "spp": a.spp, "strong": a.strong, "ps": os.environ.get("RT_PS_PIPELINE", "-1"),
-                       "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "per_rank": out,
-                       "predicted_efficiency_without_gather": {n: round(v["mrays_s_per_gpu"] / base, 3) for n, v in out.items()}})
+    ns = [int(x) for x in a.ns.split(",")]
+    full_cost = None
+    res = {}
+    for deal in a.deal.split(","):
+        out = {}
+        for n in ns:
+            spp = a.spp if a.strong else a.spp * n
+            cap = ((a.w + 7) // 8) * ((a.h + 7) // 8) * 64
+            buf = torch.zeros(cap, dtype=torch.int32, device="cuda")
+            if deal == "balanced":
+                tiles, off = rt.tile_deal(a.w, a.h, n, full_cost if (full_cost is not None and full_cost.size) else None)
+            ranks = range(n) if a.ranks == "all" else [n - 1]
+            per = []
+            for k in ranks:
+                if deal == "balanced":
+                    mine = tiles[off[k]:off[k + 1]]
+                    render = lambda r, spp_, fr, s, mine=mine: r.render_shard_tiles(buf, mine, spp=spp_, depth=a.depth, frame=fr, stream=s)
+                else:
+                    render = lambda r, spp_, fr, s, k=k, n=n: r.render_shard(buf, k, n, spp=spp_, depth=a.depth, frame=fr, stream=s)
+                t, cost = time_share(scene, a, spp, a.frames, render)
+                if n == 1 and deal == "interleaved" and full_cost is None:
+                    full_cost = cost.astype(np.uint32)
+                per.append(t)
+            worst = max(per, key=lambda x: x["ms"])
+            out[n] = {"ms_per_frame_max_rank": worst["ms"], "ms_per_frame_mean_rank": round(float(np.mean([p["ms"] for p in per])), 4),
+                      "in_flight_max_rank": worst["in_flight"], "per_rank": per}
+            print(deal, n, json.dumps({k: v for k, v in out[n].items() if k != "per_rank"}), flush=True)
+        base = out[ns[0]]["ms_per_frame_max_rank"] * ns[0] if a.strong else out[ns[0]]["ms_per_frame_max_rank"]
+        eff = {n: round((base / (v["ms_per_frame_max_rank"] * n)) if a.strong else (base / v["ms_per_frame_max_rank"]), 3)
+               for n, v in out.items()}
+        res[deal] = {"per_n": out, "predicted_efficiency_without_gather": eff}
+    line = json.dumps({"scene": a.scene, "depth": a.depth, "spp": a.spp, "strong": a.strong, "size": [a.w, a.h],
+                       "ps": os.environ.get("RT_PS_PIPELINE", "-1"), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                       "deals": res})
     print(line, flush=True)
     if a.out:
-        with open(a.out, "a") as f:
-            f.write(line + "\n")
+        with open(a.out, "a") as fo:
+            fo.write(line + "\n")
 
 
 if __name__ == "__main__":

@@ -331,8 +331,13 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (d->bvh_nodes && d->bvh_num_nodes > kMaxNodes)
         return fail(RT_ERR_UNSUPPORTED, "prebuilt BVH with more than 2^24 nodes (24-bit child index)");
     int32_t bvh_kind = d->bvh_kind;
-    if (const char *e = std::getenv("RT_BVH")) bvh_kind = std::strcmp(e, "sbvh") == 0 ? RT_BVH_SBVH : RT_BVH_PLAIN;
     if (bvh_kind != RT_BVH_PLAIN && bvh_kind != RT_BVH_SBVH) return fail(RT_ERR_INVALID, "unknown bvh_kind");
+    // RT_BVH (plain / sbvh) picks the tree only where the caller left the default
+    if (const char *e = std::getenv("RT_BVH")) {
+        if (std::strcmp(e, "sbvh") != 0 && std::strcmp(e, "plain") != 0)
+            return fail(RT_ERR_INVALID, std::string("RT_BVH must be 'plain' or 'sbvh', not '") + e + "'");
+        if (bvh_kind == RT_BVH_PLAIN) bvh_kind = std::strcmp(e, "sbvh") == 0 ? RT_BVH_SBVH : RT_BVH_PLAIN;
+    }
     int rc = ensure_device(d->device);
     if (rc != RT_OK) return rc;
 

@@ -235,12 +235,18 @@ struct Sbvh {
                 }
             }
             const bool must = R.size() > 64;   // keep leaves within the kernels' 255-primitive word
-            if (s.axis < 0 || (!(s.cost < leaf_cost) && !must)) {
+            if (!must && (s.axis < 0 || !(s.cost < leaf_cost))) {
                 leaves.push_back({job.ni, std::move(R)});
                 continue;
             }
             std::vector<Ref> L, Rr;
-            if (!s.spatial) {
+            if (s.axis < 0) {
+                // no split plane separates the centroids (many references share one centroid):
+                // halve the references by index, so every leaf stays within the limit
+                const size_t h = R.size() / 2;
+                L.assign(R.begin(), R.begin() + (long)h);
+                Rr.assign(R.begin() + (long)h, R.end());
+            } else if (!s.spatial) {
                 for (Ref &r : R) (0.5f * (r.box.mn[s.axis] + r.box.mx[s.axis]) < s.pos ? L : Rr).push_back(r);
             } else {
                 for (Ref &r : R) {
@@ -254,7 +260,12 @@ struct Sbvh {
                     else (ha ? L : Rr).push_back(ha ? a : b);
                 }
             }
-            if (L.empty() || Rr.empty()) { leaves.push_back({job.ni, std::move(R)}); continue; }
+            if (L.empty() || Rr.empty()) {
+                if (!must) { leaves.push_back({job.ni, std::move(R)}); continue; }
+                const size_t h = R.size() / 2;   // a split that separated nothing: halve by index
+                L.assign(R.begin(), R.begin() + (long)h);
+                Rr.assign(R.begin() + (long)h, R.end());
+            }
             const uint32_t left = (uint32_t)nodes.size();
             nodes.resize(nodes.size() + 2);
             nodes[job.ni].leftFirst = left;

@@ -69,3 +69,22 @@ def test_sbvh_splits_references_on_the_big_scene(rt):
     assert len(prims) < info["num_refs"] <= 2 * len(prims)
     assert info["depth"] <= 64 and info["max_leaf"] <= 255 and info["nodes_used"] < (1 << 24)
     check_structure(nodes, idx, len(prims))
+
+
+def test_sbvh_splits_coincident_triangles_into_bounded_leaves(rt):
+    """300 copies of one triangle share one centroid, so no SAH plane separates them: the
+    builder halves such sets by index (leaves stay within the kernels' 255-primitive word,
+    above 64 references a split is forced) instead of failing the scene."""
+    light = rt.sphere((0, 4, -2), 0.5, 0)
+    tris = [rt.triangle((0, 0, 1), (1, 0, 1), (0, 1, 1), 0) for _ in range(300)]
+    nodes, idx, info = rt.build_sbvh_host([light] + tris)
+    check_structure(nodes, idx, 301)
+    assert info["max_leaf"] <= 64
+
+
+def test_rt_bvh_environment_value_is_checked(rt, monkeypatch):
+    """RT_BVH takes 'plain' or 'sbvh' only (a typo is an error, not a silent plain tree)."""
+    monkeypatch.setenv("RT_BVH", "SBVH")
+    with pytest.raises(rt.RTError) as e:   # refused before any device call
+        rt.Scene.recipe("teapotF")
+    assert e.value.code == rt.RT_ERR_INVALID and "RT_BVH" in str(e.value)

@@ -153,6 +153,12 @@ struct TraceArgs {
 RT_DECLARE_LAUNCHERS(kcore)
 RT_DECLARE_LAUNCHERS(kext)
 #undef RT_DECLARE_LAUNCHERS
+// RT_PT_SORT: reorder a bounce level's queue (P.queue_in, P.level) by direction octant + origin
+// cell into `sorted` (same segment layout; the level's queue counts are rewritten); work =
+// pt_sort_work_bytes(), keys = 2 B per path of the batch
+void launch_pt_sort(const SceneView &S, const PathArgs &P, uint32_t *sorted, uint32_t *work, uint16_t *keys,
+                    uint32_t num_cus, hipStream_t st);
+size_t pt_sort_work_bytes();
 // where: per global tile (shard << 24 | local tile) of an explicit deal; nullptr = interleaved
 void launch_assemble(const uint32_t *gathered, uint32_t cap, uint32_t nshards, const uint32_t *where, uint32_t tiles_x,
                      uint32_t ntiles, uint32_t W, uint32_t H, uint32_t *out, hipStream_t st);

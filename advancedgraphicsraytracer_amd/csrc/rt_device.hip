@@ -69,6 +69,7 @@ struct rt_scene {
                                     // one compact screen region of 1/8 of the frame's cost (L2 locality)
     int32_t heavy_split = -1;       // primary+shadow frames: the costliest tiles run as two half-tile
                                     // waves (RT_SPLIT_HEAVY = count; -1: ntiles / 32)
+    uint32_t pt_sort_levels = 0;    // bounce levels 1..n reordered by direction octant + origin cell (RT_PT_SORT)
     uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per slot (two when pipelined): 12 GB
                                               // of the 288 GB HBM holds all 16 spp of a 1080p depth-10 frame
     bool pt_pipeline = true;        // sample batches alternate path-state slots and streams
@@ -620,6 +621,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_PT_WAVEFRONT")) s->pt_wavefront = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_DYNAMIC")) s->pt_dynamic = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_LANES")) s->pt_lanes = std::atoi(e) != 0;
+    if (const char *e = std::getenv("RT_PT_SORT")) s->pt_sort_levels = (uint32_t)std::max(0, std::atoi(e));
     // RT_PT_DRAIN_LEVEL / RT_PT_MEM_MB: wavefront drain level and path-state budget (A/B runs)
     if (const char *e = std::getenv("RT_PT_DRAIN_LEVEL")) s->pt_drain_level = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_DRAIN_ROUNDS")) s->pt_drain_rounds = std::max(0.0, std::atof(e));
@@ -797,7 +799,10 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     const uint64_t seg_cap = ((np / 64u + kQueueSegs - 1) / kQueueSegs + 1) * 64u;
     const size_t qbytes = (size_t)seg_cap * kQueueSegs * 4u;
     const size_t cbytes = (size_t)(F.depth + 1) * (2u * kQueueSegs) * 64u;   // queue counts + head counters
-    const size_t need = (size_t)(np * (per_path - 8u) + 2 * qbytes + cbytes + 4096u);
+    // RT_PT_SORT: a third queue (the sorted level), 2-B keys per path and the sort's counters
+    const bool sorting = s->pt_sort_levels > 0 && F.depth >= 2;
+    const size_t sort_bytes = sorting ? qbytes + (size_t)np * 2u + pt_sort_work_bytes() + 3 * 256u : 0;
+    const size_t need = (size_t)(np * (per_path - 8u) + 2 * qbytes + cbytes + 4096u) + sort_bytes;
     if (!r->d_sum) {   // one float4 per pixel of the whole frame (a shard uses its first npix)
         const size_t tiles = (size_t)((r->W + 7) / 8) * ((r->H + 7) / 8);
         HIP_TRY(hipMalloc(&r->d_sum, tiles * 64u * sizeof(float4)));
@@ -845,6 +850,9 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         P.qhead = P.qcount + (size_t)(F.depth + 1) * kQueueSegs * 16u;
         P.dynamic = s->pt_dynamic ? 1 : 0;
         P.rec = reinterpret_cast<float4 *>(take((size_t)(F.depth - 1) * np * 32u));
+        uint32_t *qsorted = sorting ? reinterpret_cast<uint32_t *>(take(qbytes)) : nullptr;
+        uint16_t *skeys = sorting ? reinterpret_cast<uint16_t *>(take((size_t)np * 2u)) : nullptr;
+        uint32_t *swork = sorting ? reinterpret_cast<uint32_t *>(take(pt_sort_work_bytes())) : nullptr;
         // per-path radiance, indexed (sample - s0) * npix + pixel
         P.result = pipe ? r->d_res[par] + (size_t)s0 * npix : reinterpret_cast<float4 *>(take(np * 16u));
         P.sum = r->d_sum;
@@ -858,6 +866,10 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
             P.level = level;
             P.queue_in = (level & 1u) ? q1 : q0;
             P.queue_out = (level & 1u) ? q0 : q1;
+            if (sorting && level >= 1 && level <= s->pt_sort_levels) {   // reorder this level's queue
+                launch_pt_sort(view, P, qsorted, swork, skeys, s->num_cus, X);
+                P.queue_in = qsorted;
+            }
             int resident = 0;
             if (level > 0 && s->pt_lanes) {             // incoherent levels: the lane state machine
                 if (s->ext) kext::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, X);

@@ -474,6 +474,8 @@ def test_frame_kernel_name(rt):
     ("cfg3", 64, 48, 2, 32, {}),                                # the deepest Trace (32): meta bits, records
     ("cfg3", 136, 80, 4, 4, {"RT_PT_LANES": "0"}),              # chunk kernel at every level
     ("teapotF", 200, 120, 1, 10, {"RT_PT_LANES": "0", "RT_PT_DYNAMIC": "0"}),   # static chunks
+    ("cfg5", 160, 96, 4, 10, {"RT_PT_SORT": "3"}),              # levels 1-3 reordered (octant + cell)
+    ("cfg3", 136, 80, 4, 4, {"RT_PT_SORT": "9", "RT_PT_MEM_MB": "2"}),   # every level sorted, several batches
 ])
 def test_wavefront_equals_one_kernel_path_tracer(rt, torch, monkeypatch, recipe, W, H, spp, depth, env):
     """The wavefront path tracer (k_pt_level + k_pt_finish: compaction between bounce

@@ -79,6 +79,9 @@ struct rt_scene {
     int32_t ps_pipeline = -1;       // primary+shadow frames overlap: -1 timed per renderer (auto),
                                     // 0 never, 1 always (RT_PS_PIPELINE)
     uint32_t ps_depth = 2;          // frames in flight when forced (RT_PS_DEPTH, 2-4)
+    float tune_delay_ms = 100.0f;   // GPU time a parameter set runs before its timed choices start
+                                    // (RT_TUNE_DELAY_MS): the clocks ramp over ~0.1 s, and choices
+                                    // timed on the first frames at low clocks came out wrong
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
     void *d_xprims = nullptr, *d_tex = nullptr, *d_pairs = nullptr, *d_pairs48 = nullptr, *d_words = nullptr;
     void *d_scratch = nullptr;  // staging for the host-pointer batched calls
@@ -153,6 +156,13 @@ struct rt_renderer {
     hipEvent_t ps_fin[5] = {};
     bool ps_fin_set[5] = {};
     uint32_t ps_count = 0;
+    // tuning gate: the timed choices (camera walk, split order, frames in flight) of a parameter
+    // set start once its frames have run tune_delay_ms of GPU time -- an event at its first frame
+    // and a probe every 8 frames, read without blocking
+    uint64_t gate_key = 0;
+    int gate_state = 0;             // 0 start, 1 running, 2 probe recorded, 3 open
+    uint32_t gate_frames = 0;
+    hipEvent_t gate_ev[2] = {};
     // per-sample values of sample-split frames (FrameArgs::samples)
     void *d_samples = nullptr;
     size_t samples_bytes = 0;
@@ -638,6 +648,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_PS_PIPELINE")) s->ps_pipeline = std::max(-1, std::min(1, std::atoi(e)));
     if (const char *e = std::getenv("RT_PS_BUFFERS")) s->ps_buffers = (uint32_t)std::max(2, std::min(5, std::atoi(e)));
     if (const char *e = std::getenv("RT_PS_DEPTH")) s->ps_depth = (uint32_t)std::max(2, std::min(4, std::atoi(e)));
+    if (const char *e = std::getenv("RT_TUNE_DELAY_MS")) s->tune_delay_ms = (float)std::max(0.0, std::atof(e));
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
@@ -979,19 +990,9 @@ std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const uint32_t *map,
     return out;
 }
 
-int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt_frame_params *p, int walk_phase,
-                    bool split_ok, int &split_timed) {
+int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, bool split_ok, bool gate_open,
+                    int &split_timed) {
     split_timed = -1;
-    uint64_t key = 1469598103934665603ull;
-    auto mix = [&](const void *d, size_t n) {
-        const unsigned char *c = static_cast<const unsigned char *>(d);
-        for (size_t i = 0; i < n; ++i) key = (key ^ c[i]) * 1099511628211ull;
-    };
-    mix(cam, sizeof(*cam));
-    mix(&p->width, sizeof(uint32_t) * 4);   // width height spp depth
-    mix(&p->mode, sizeof(uint32_t));
-    mix(&F.shard, sizeof(uint32_t) * 2);    // shard nshards
-    if (F.tile_map) mix(&r->map_hash, sizeof(r->map_hash));   // an explicit deal's tile list
     const uint32_t n = F.ntiles_local;
     if (key != r->order_key || n != r->order_n) {
         r->order_key = key;
@@ -1068,7 +1069,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
             for (int i = 0; i < 4; ++i) HIP_TRY(hipEventElapsedTime(&r->split_ms[i], r->sev[2 * i], r->sev[2 * i + 1]));
             r->use_split = split = r->split_ms[1] + r->split_ms[3] < r->split_ms[0] + r->split_ms[2];
             r->split_phase = -1;
-        } else if (r->split_phase >= 0) {
+        } else if (r->split_phase >= 0 && gate_open) {
             split = r->split_phase & 1;
             split_timed = r->split_phase++;
         }
@@ -1079,6 +1080,46 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, const rt_camera *cam, const rt
 }
 
 constexpr int kPsGroup = 8;   // frames per timed group of the overlap decision
+
+// the parameter set a frame belongs to (the tuned choices and the tile order are per set)
+uint64_t param_key(const rt_renderer *r, const FrameArgs &F, const rt_camera *cam, const rt_frame_params *p) {
+    uint64_t key = fnv1a(cam, sizeof(*cam));
+    key = fnv1a(&p->width, sizeof(uint32_t) * 4, key);   // width height spp depth
+    key = fnv1a(&p->mode, sizeof(uint32_t), key);
+    key = fnv1a(&F.shard, sizeof(uint32_t) * 2, key);    // shard nshards
+    if (F.tile_map) key = fnv1a(&r->map_hash, sizeof(r->map_hash), key);   // an explicit deal's tile list
+    return key;
+}
+
+// true once this parameter set's frames have run tune_delay_ms of GPU time (never blocks)
+int tune_gate(rt_renderer *r, uint64_t key, hipStream_t st, bool &open) {
+    const float delay = r->scene->tune_delay_ms;
+    if (key != r->gate_key) {
+        r->gate_key = key;
+        r->gate_state = 0;
+    }
+    if (delay <= 0.0f) r->gate_state = 3;
+    if (r->gate_state == 3) { open = true; return RT_OK; }
+    open = false;
+    if (!r->gate_ev[0])
+        for (auto &e : r->gate_ev) HIP_TRY(hipEventCreate(&e));
+    if (r->gate_state == 0) {
+        HIP_TRY(hipEventRecord(r->gate_ev[0], st));
+        r->gate_state = 1;
+        r->gate_frames = 0;
+    } else if (r->gate_state == 1) {
+        if (++r->gate_frames % 8 == 0) {
+            HIP_TRY(hipEventRecord(r->gate_ev[1], st));
+            r->gate_state = 2;
+        }
+    } else if (hipEventQuery(r->gate_ev[1]) == hipSuccess) {   // state 2: the probe has run
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, r->gate_ev[0], r->gate_ev[1]));
+        r->gate_state = ms >= delay ? 3 : 1;
+        open = r->gate_state == 3;
+    }
+    return RT_OK;
+}
 
 int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
                   uint32_t *out, int packed, void *stream, const uint32_t *tiles = nullptr, uint32_t ntiles_map = 0) {
@@ -1171,6 +1212,9 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     }
     FrameLaunch L{mode, md, tex, lds_kind, grid, block, lds, st};
     SceneView view = s->view;
+    const uint64_t pkey = param_key(r, F, cam, p);
+    bool gate_open = false;
+    if (int rc = tune_gate(r, pkey, st, gate_open); rc != RT_OK) return rc;
     // camera-ray walk (only the global-node primary+shadow kernel has both)
     const bool walk_kernel = mode == RT_MODE_PATH && md == 1 && lds_kind == 0 && !s->ext;
     int timed = -1;   // tev pair recorded around this launch
@@ -1178,7 +1222,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     const bool walk_pending = walk_kernel && s->walk == RT_WALK_AUTO && r->tune < 4;
     if (walk_kernel) {
         if (s->walk == RT_WALK_WAVE) view.wave_primary = 1;
-        else if (s->walk == RT_WALK_AUTO) {
+        else if (s->walk == RT_WALK_AUTO && (gate_open || r->tune >= 3)) {
             if (r->tune < 3) {
                 if (!r->tev[0])
                     for (auto &e : r->tev) HIP_TRY(hipEventCreate(&e));
@@ -1201,8 +1245,8 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     if (s->tile_order) {
         // half-tile units: primary+shadow frames of the global-node kernel, whole-tile units only
         const bool split_ok = mode == RT_MODE_PATH && md == 1 && lds_kind == 0 && F.nchunks <= 1;
-        const int rc = tile_order_step(r, F, cam, p, timed == 0 ? 0 : timed == 2 ? 1 : walk_decided ? 2 : walk_pending ? 3 : -1,
-                                       split_ok, split_timed);
+        const int rc = tile_order_step(r, F, pkey, timed == 0 ? 0 : timed == 2 ? 1 : walk_decided ? 2 : walk_pending ? 3 : -1,
+                                       split_ok, gate_open, split_timed);
         if (rc != RT_OK) return rc;
         if (lds_kind == 0) L.grid = dim3((F.nunits + 3) / 4);
     }
@@ -1235,15 +1279,21 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     // frames in flight for this frame: 0 = serial, else 2..4 renderer streams
     uint32_t depth_k = (ps_ok && s->ps_pipeline == 1) ? s->ps_depth : 0u;
     int ps_ev0 = -1, ps_ev1 = -1;   // pev recorded on the caller's stream before / after this frame
-    if (ps_ok && s->ps_pipeline < 0) {
+    // 4 frames in flight are a candidate only for frames of a few rounds of resident waves (a
+    // multi-GPU rank's small shard); a throughput-bound frame (TEAPOT-F 1080p, 8 rounds) lost
+    // with them (0.1035 -> 0.114 ms) and the timing only risked picking them
+    const bool deep_ok = F.nunits <= 3u * 4u * 5u * s->num_cus;
+    if (ps_ok && s->ps_pipeline < 0 && !gate_open) depth_k = 0;   // timing not started: serial
+    if (ps_ok && s->ps_pipeline < 0 && gate_open) {
         constexpr int G = kPsGroup;
-        static constexpr uint32_t kGroupDepth[6] = {0, 2, 4, 4, 2, 0};
+        const uint32_t kGroupDepth[6] = {0, 2, deep_ok ? 4u : 2u, deep_ok ? 4u : 2u, 2, 0};
         if (r->ps_phase > 0 && r->ps_phase < 6 * G && r->frames != r->ps_last + 1) r->ps_phase = 0;   // interrupted
         if (r->ps_phase == 6 * G) {
             HIP_TRY(hipEventSynchronize(r->pev[11]));
             for (int g = 0; g < 6; ++g) HIP_TRY(hipEventElapsedTime(&r->ps_ms[g], r->pev[2 * g], r->pev[2 * g + 1]));
             const float t0 = r->ps_ms[0] + r->ps_ms[5], t2 = r->ps_ms[1] + r->ps_ms[4], t4 = r->ps_ms[2] + r->ps_ms[3];
-            r->ps_use = (t4 < t2 && t4 < t0) ? 4u : (t2 < t0 ? 2u : 0u);
+            if (deep_ok) r->ps_use = (t4 < t2 && t4 < t0) ? 4u : (t2 < t0 ? 2u : 0u);
+            else r->ps_use = 0.25f * (t2 + t4) < 0.5f * t0 ? 2u : 0u;   // groups 1-4 all ran 2 in flight
             r->ps_phase = -1;
         }
         if (r->ps_phase >= 0) {
@@ -1629,6 +1679,8 @@ int rt_renderer_destroy(rt_renderer *r) {
     for (auto &e : r->sev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : r->pev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto &e : r->gate_ev)
         if (e) (void)hipEventDestroy(e);
     if (r->ps_join) (void)hipEventDestroy(r->ps_join);
     for (int b = 0; b < 5; ++b) {

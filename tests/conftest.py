@@ -9,6 +9,10 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))   # tests are allowed to use th
 
 REFERENCE = "/root/reference"
 
+# the renderers' timed choices (camera walk, split order, frames in flight) start after 100 ms
+# of GPU time by default (clock ramp); tests exercise them on their first frames
+os.environ.setdefault("RT_TUNE_DELAY_MS", "0")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (runs on the MI355X box)")

@@ -772,8 +772,6 @@ def test_treelet_lane_kernel_equals_default(rt, torch, monkeypatch, recipe, spp,
     assert np.array_equal(s_a.bvh()[0], s_b.bvh()[0])     # rt_scene_copy_bvh keeps the reference order
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("recipe", ["teapotF", "mig16", "cfg3"])
 def assert_ties(rt, oracle, recipe, rays, t, obj, wobj):
     """Every ray whose closest-hit id differs between two trees hits BOTH primitives at the same
     distance t (a tie, decided by visiting order, template/scene.h:298-318): each id alone, with
@@ -786,6 +784,8 @@ def assert_ties(rt, oracle, recipe, rays, t, obj, wobj):
             assert so[0] >= 0 and st_.view(np.uint32)[0] == t.view(np.uint32)[i], (i, pid, st_[0], t[i])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("recipe", ["teapotF", "mig16", "cfg3"])
 def test_sbvh_scene_matches_plain_oracle_except_ties(rt, oracle, scenes, recipe):
     """The opt-in SBVH (RT_BVH_SBVH) on the GPU: closest-hit t bit-exact against the oracle's
     plain BVH on camera and random rays; ids identical except exact-distance ties, each one

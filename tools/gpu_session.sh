@@ -28,6 +28,9 @@ for s in "$@"; do
             step shard_cfg5 600 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --deal interleaved,balanced --ranks last --out gpurun_out/shard_time.jsonl
             step shard_cfg3 600 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg3 --depth 4 --spp 4 --warm 6 --frames 6 --deal interleaved,balanced --ranks last --out gpurun_out/shard_time.jsonl ;;
         region) step region 300 python tools/timed_region.py --out gpurun_out/timed_region.jsonl ;;
+        sortab)
+            step sortab_c5 600 env GPU_MAX_HW_QUEUES=8 python tools/knob_ab.py --scene cfg5 --spp 16 --depth 10 --var RT_PT_SORT=0 --var RT_PT_SORT=1 --var RT_PT_SORT=3 --check --out gpurun_out/knob_ab.jsonl
+            step sortab_c3 600 env GPU_MAX_HW_QUEUES=8 python tools/knob_ab.py --scene cfg3 --spp 4 --depth 4 --var RT_PT_SORT=0 --var RT_PT_SORT=1 --var RT_PT_SORT=3 --check --out gpurun_out/knob_ab.jsonl ;;
         benchcfg)
             step bench_cfg3 300 python bench.py --config 3 --steps 10 --warmup 2 --no-cpu-baseline
             step bench_cfg4 300 python bench.py --config 4 --steps 30 --warmup 5 --no-cpu-baseline

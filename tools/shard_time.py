@@ -27,15 +27,19 @@ def time_share(scene, a, spp, frames, render):
     """warm-up frames (walk timing, tile order, frames-in-flight timing), then `frames` timed."""
     r = rt.Renderer(scene, a.w, a.h)
     st = torch.cuda.Stream()
-    for f in range(a.warm):
+    f, t0 = 0, time.perf_counter()
+    while f < a.warm or time.perf_counter() - t0 < a.warm_seconds:   # past the renderer's tuning gate
         render(r, spp, f, st.cuda_stream)
+        f += 1
+        if f % 20 == 0:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     c0 = r.counters()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     with torch.cuda.stream(st):
         ev[0].record()
         for f in range(frames):
-            render(r, spp, a.warm + f, st.cuda_stream)
+            render(r, spp, 100000 + f, st.cuda_stream)
         ev[1].record()
     torch.cuda.synchronize()
     c1 = r.counters()
@@ -58,7 +62,9 @@ def main():
     ap.add_argument("--w", type=int, default=1920)
     ap.add_argument("--h", type=int, default=1080)
     ap.add_argument("--warm", type=int, default=80, help="untimed frames per renderer (walk, tile order and "
-                    "frames-in-flight timing: ~60 frames)")
+                    "frames-in-flight timing: ~60 frames after the tuning gate)")
+    ap.add_argument("--warm-seconds", type=float, default=0.4, help="... and at least this much wall time (the "
+                    "renderer's timed choices start after 100 ms of GPU time, RT_TUNE_DELAY_MS)")
     ap.add_argument("--strong", action="store_true", help="the config's spp per shard (one frame split N ways)")
     ap.add_argument("--spp", type=int, default=1, help="samples per pixel of the whole frame (strong) / per GPU (weak)")
     ap.add_argument("--ns", default="1,2,4,8")

@@ -107,13 +107,14 @@ struct rt_renderer {
     uint64_t order_key = 0;
     int order_state = 0;        // 0 idle, 1 costs recorded, 2 order active
     uint32_t order_split = 0;   // leading tiles of the split order that run as two half-tile units
-    int split_phase = -1;       // -1 decided / not tried; 0..3 timing frames (plain, split, plain, split)
+    int split_phase = -1;       // -1 decided / not tried; 0 .. 4 kTuneGroup - 1 timing frames in groups
+                                // (plain, split, split, plain), 4 kTuneGroup decide
     bool use_split = false;     // the split order measured faster
     hipEvent_t sev[8] = {};     // split timing: events 2i, 2i+1 around timing frame i
     float split_ms[4] = {};
-    int tune = 0;
+    int tune = 0;                   // camera walk: 0 warm-up, 1 .. kWalkTimed timed frames, kTuneDecide, kTuneDone
     bool wave = false;
-    hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t tev[8] = {};         // walk timing: events 2g, 2g + 1 around group g
     // wavefront path tracer (PathArgs): two path-state slots (state, records, queues), grown on
     // demand, each owned by one of the renderer's two path streams.  Sample batches alternate
     // between them, so one batch's (or the next frame's) level 0 fills the CUs that the other
@@ -181,6 +182,14 @@ namespace {
 
 inline float ubits(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 inline float ibits(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
+
+// The timed choices between two variants (camera walk, split order) time four groups of
+// kTuneGroup frames in the order A, B, B, A (a clock drift over the groups cancels) and keep
+// the faster -- single frames were too noisy to decide on (ranks with equal work came out 35 %
+// apart in round-3 shard timings)
+constexpr int kTuneGroup = 4;
+constexpr int kWalkTimed = 4 * kTuneGroup;
+constexpr int kTuneDecide = 1 + kWalkTimed, kTuneDone = kTuneDecide + 1;
 
 uint32_t pick_stack(uint32_t depth) {   // entries needed <= tree depth; round up to 8
     uint32_t need = depth < 2 ? 2 : depth;
@@ -790,7 +799,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     rt_scene *s = r->scene;
     // camera rays of level 0 take the wave-coherent walk when the scene forces it, or when
     // the renderer's primary+shadow frames timed it faster (RT_WALK_AUTO)
-    view.wave_primary = !s->has_cubes && (s->walk == RT_WALK_WAVE || (s->walk == RT_WALK_AUTO && r->tune == 4 && r->wave));
+    view.wave_primary = !s->has_cubes && (s->walk == RT_WALK_WAVE || (s->walk == RT_WALK_AUTO && r->tune == kTuneDone && r->wave));
     const uint64_t npix = (uint64_t)F.ntiles_local * 64u;
     // pipelined: per-sample results of the whole frame in a frame-level buffer (two by frame
     // parity, up to 2 GB each); the serial path keeps them per batch with a running sum
@@ -991,8 +1000,8 @@ std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const uint32_t *map,
 }
 
 int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, bool split_ok, bool gate_open,
-                    int &split_timed) {
-    split_timed = -1;
+                    int &split_ev0, int &split_ev1) {
+    split_ev0 = split_ev1 = -1;
     const uint32_t n = F.ntiles_local;
     if (key != r->order_key || n != r->order_n) {
         r->order_key = key;
@@ -1064,14 +1073,17 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
     }
     if (r->order_state == 2) {
         bool split = r->use_split;
-        if (r->split_phase == 4) {                                     // decide after the 4 timed frames
+        if (r->split_phase == 4 * kTuneGroup) {                        // decide after the timed groups
             HIP_TRY(hipEventSynchronize(r->sev[7]));
             for (int i = 0; i < 4; ++i) HIP_TRY(hipEventElapsedTime(&r->split_ms[i], r->sev[2 * i], r->sev[2 * i + 1]));
-            r->use_split = split = r->split_ms[1] + r->split_ms[3] < r->split_ms[0] + r->split_ms[2];
+            r->use_split = split = r->split_ms[1] + r->split_ms[2] < r->split_ms[0] + r->split_ms[3];
             r->split_phase = -1;
         } else if (r->split_phase >= 0 && gate_open) {
-            split = r->split_phase & 1;
-            split_timed = r->split_phase++;
+            const int g = r->split_phase / kTuneGroup, i = r->split_phase % kTuneGroup;   // plain, split, split, plain
+            split = g == 1 || g == 2;
+            split_ev0 = i == 0 ? 2 * g : -1;
+            split_ev1 = i == kTuneGroup - 1 ? 2 * g + 1 : -1;
+            ++r->split_phase;
         }
         F.order = split ? r->d_order + n : r->d_order;
         F.nunits = F.ntiles_local * F.nchunks + (split ? r->order_split : 0u);   // split only with nchunks 1
@@ -1217,36 +1229,41 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     if (int rc = tune_gate(r, pkey, st, gate_open); rc != RT_OK) return rc;
     // camera-ray walk (only the global-node primary+shadow kernel has both)
     const bool walk_kernel = mode == RT_MODE_PATH && md == 1 && lds_kind == 0 && !s->ext;
-    int timed = -1;   // tev pair recorded around this launch
+    int walk_ev0 = -1, walk_ev1 = -1;   // tev recorded before / after this launch
+    int cost_map = -1;                  // this frame records the tile costs under walk 0 / 1
     bool walk_decided = false;
-    const bool walk_pending = walk_kernel && s->walk == RT_WALK_AUTO && r->tune < 4;
+    const bool walk_pending = walk_kernel && s->walk == RT_WALK_AUTO && r->tune < kTuneDone;
     if (walk_kernel) {
         if (s->walk == RT_WALK_WAVE) view.wave_primary = 1;
-        else if (s->walk == RT_WALK_AUTO && (gate_open || r->tune >= 3)) {
-            if (r->tune < 3) {
+        else if (s->walk == RT_WALK_AUTO && (gate_open || r->tune >= kTuneDecide)) {
+            if (r->tune < kTuneDecide) {
                 if (!r->tev[0])
                     for (auto &e : r->tev) HIP_TRY(hipEventCreate(&e));
-                if (r->tune == 1) timed = 0;                       // lane walk
-                if (r->tune == 2) { timed = 2; view.wave_primary = 1; }
+                if (r->tune >= 1) {   // groups lane, wave, wave, lane
+                    const int g = (r->tune - 1) / kTuneGroup, i = (r->tune - 1) % kTuneGroup;
+                    view.wave_primary = (g == 1 || g == 2) ? 1 : 0;
+                    if (i == 0) walk_ev0 = 2 * g;
+                    if (i == kTuneGroup - 1) walk_ev1 = 2 * g + 1;
+                    if (i == 0 && g < 2) cost_map = g;   // each walk's tile costs, on its first frame
+                }
                 ++r->tune;
-            } else if (r->tune == 3) {                             // decide once, after both timed frames
-                float tl = 0, tw = 0;
-                HIP_TRY(hipEventSynchronize(r->tev[3]));
-                HIP_TRY(hipEventElapsedTime(&tl, r->tev[0], r->tev[1]));
-                HIP_TRY(hipEventElapsedTime(&tw, r->tev[2], r->tev[3]));
-                r->wave = tw < tl;
-                r->tune = 4;
+            } else if (r->tune == kTuneDecide) {                   // decide once, after the timed groups
+                float t[4] = {};
+                HIP_TRY(hipEventSynchronize(r->tev[7]));
+                for (int g = 0; g < 4; ++g) HIP_TRY(hipEventElapsedTime(&t[g], r->tev[2 * g], r->tev[2 * g + 1]));
+                r->wave = t[1] + t[2] < t[0] + t[3];
+                r->tune = kTuneDone;
                 walk_decided = true;
             }
-            if (r->tune == 4) view.wave_primary = r->wave ? 1 : 0;
+            if (r->tune == kTuneDone) view.wave_primary = r->wave ? 1 : 0;
         }
     }
-    int split_timed = -1;   // sev pair recorded around this launch
+    int split_ev0 = -1, split_ev1 = -1;   // sev recorded before / after this launch
     if (s->tile_order) {
         // half-tile units: primary+shadow frames of the global-node kernel, whole-tile units only
         const bool split_ok = mode == RT_MODE_PATH && md == 1 && lds_kind == 0 && F.nchunks <= 1;
-        const int rc = tile_order_step(r, F, pkey, timed == 0 ? 0 : timed == 2 ? 1 : walk_decided ? 2 : walk_pending ? 3 : -1,
-                                       split_ok, gate_open, split_timed);
+        const int rc = tile_order_step(r, F, pkey, cost_map >= 0 ? cost_map : walk_decided ? 2 : walk_pending ? 3 : -1,
+                                       split_ok, gate_open, split_ev0, split_ev1);
         if (rc != RT_OK) return rc;
         if (lds_kind == 0) L.grid = dim3((F.nunits + 3) / 4);
     }
@@ -1275,7 +1292,8 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     // (sample-split frames -- a multi-GPU rank's shard at spp N -- store their samples anyway;
     // overlapped, they go to the result buffers instead of d_samples)
     const bool ps_ok = s->ps_pipeline != 0 && mode == RT_MODE_PATH && md == 1 && lds_kind == 0 &&
-                       timed < 0 && split_timed < 0 && !F.tile_cost && !walk_pending && ps_bytes <= (2ull << 30);
+                       split_ev0 < 0 && split_ev1 < 0 && r->split_phase < 0 && !F.tile_cost && !walk_pending &&
+                       ps_bytes <= (2ull << 30);
     // frames in flight for this frame: 0 = serial, else 2..4 renderer streams
     uint32_t depth_k = (ps_ok && s->ps_pipeline == 1) ? s->ps_depth : 0u;
     int ps_ev0 = -1, ps_ev1 = -1;   // pev recorded on the caller's stream before / after this frame
@@ -1340,13 +1358,13 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         F.samples = r->ps_res[buf];
     }
     if (ps_ok) r->ps_prev = depth_k;
-    if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed], st));
-    if (split_timed >= 0) HIP_TRY(hipEventRecord(r->sev[2 * split_timed], st));
+    if (walk_ev0 >= 0) HIP_TRY(hipEventRecord(r->tev[walk_ev0], st));
+    if (split_ev0 >= 0) HIP_TRY(hipEventRecord(r->sev[split_ev0], st));
     if (s->ext) kext::launch_frame(view, F, L);
     else kcore::launch_frame(view, F, L);
     HIP_TRY(hipGetLastError());
-    if (timed >= 0) HIP_TRY(hipEventRecord(r->tev[timed + 1], st));
-    if (split_timed >= 0) HIP_TRY(hipEventRecord(r->sev[2 * split_timed + 1], st));
+    if (walk_ev1 >= 0) HIP_TRY(hipEventRecord(r->tev[walk_ev1], st));
+    if (split_ev1 >= 0) HIP_TRY(hipEventRecord(r->sev[split_ev1], st));
     if (ps_pipe) {
         HIP_TRY(hipEventRecord(r->pt_lv[lane_st], L.stream));
         HIP_TRY(hipStreamWaitEvent(st, r->pt_lv[lane_st], 0));

@@ -172,18 +172,23 @@ def cpu_baseline(args, spp):
     return out
 
 
-def companion_rate(scene, W, H, spp, depth, stream, device, warm=60, frames=300):
+def companion_rate(scene, W, H, spp, depth, stream, device, warm_s=0.4, frames=300):
     """The same workload at another frame size on a renderer of its own (BASELINE.json's
-    metric is quoted at 1280x720 and 1920x1080): warm-up frames (camera-walk, tile-order and
-    frame-overlap tuning), then `frames` timed frames between two stream events and a wall clock."""
+    metric is quoted at 1280x720 and 1920x1080): warm-up frames for warm_s seconds (the
+    renderer's timed choices -- camera walk, split order, frames in flight -- start after 100 ms
+    of GPU time and take ~100 frames), then `frames` timed frames between two stream events and a
+    wall clock."""
     r = rt.Renderer(scene, W, H)
     out = torch.zeros(W * H, dtype=torch.int32, device=f"cuda:{device}")
     sptr = stream.cuda_stream
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.cuda.stream(stream):
-        for i in range(warm):
-            r.Tick(out, spp=spp, depth=depth, frame=i, stream=sptr)
-        torch.cuda.synchronize(device)
+        warm, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < warm_s:
+            for _ in range(20):
+                r.Tick(out, spp=spp, depth=depth, frame=warm, stream=sptr)
+                warm += 1
+            torch.cuda.synchronize(device)
         c0 = r.counters()
         t0 = time.perf_counter()
         e0.record(stream)

@@ -165,6 +165,7 @@ def lib():
         "rt_renderer_overlap": ([vp, C.POINTER(C.c_int), fp], C.c_int),
         "rt_renderer_overlap_depth": ([vp, C.POINTER(C.c_int), fp], C.c_int),
         "rt_renderer_tile_costs": ([vp, C.POINTER(u32), u32, C.POINTER(u32)], C.c_int),
+        "rt_renderer_choices": ([vp, C.POINTER(C.c_int), C.POINTER(C.c_int), fp, fp], C.c_int),
         "rt_renderer_stream": ([vp, C.POINTER(vp)], C.c_int),
         "rt_frame_kernel_name": ([vp, C.POINTER(FrameParams)], C.c_char_p),
         "rt_synchronize": ([vp], C.c_int),
@@ -713,12 +714,21 @@ class Renderer:
         return st.value, [round(float(x), 4) for x in ms]
 
     def overlap_depth(self):
-        """Primary+shadow frames in flight: (depth, group ms) -- 1 serial, 2..4 overlapped, -1 not
-        decided yet; ms = the six timed groups (serial, 2, 4, 4, 2, serial in flight)."""
+        """Primary+shadow frames in flight: (depth, group ms) -- 1 serial, 2..6 overlapped, -1 not
+        decided yet; ms = the timed groups (serial, 2, 4, 6, 6, 4, 2, serial or serial, 2, 2, serial)."""
         d = C.c_int()
-        ms = np.zeros(6, np.float32)
+        ms = np.zeros(8, np.float32)
         _check(self.L.rt_renderer_overlap_depth(self.h, C.byref(d), _fptr(ms)))
         return d.value, [round(float(x), 4) for x in ms]
+
+    def choices(self):
+        """Timed choices of the current parameter set: {walk: 0 lane / 1 wave / -1, split: 1 / 0 / -1,
+        walk_ms, split_ms} (groups A, B, B, A)."""
+        w, sp = C.c_int(), C.c_int()
+        wm, sm = np.zeros(4, np.float32), np.zeros(4, np.float32)
+        _check(self.L.rt_renderer_choices(self.h, C.byref(w), C.byref(sp), _fptr(wm), _fptr(sm)))
+        return {"walk": w.value, "split": sp.value, "walk_ms": [round(float(x), 4) for x in wm],
+                "split_ms": [round(float(x), 4) for x in sm]}
 
     def tile_costs(self):
         """Per-local-tile wave cycles behind the measured tile order (empty until recorded)."""

@@ -75,10 +75,10 @@ struct rt_scene {
     bool pt_pipeline = true;        // sample batches alternate path-state slots and streams
                                     // (RT_PT_PIPELINE=0: one slot, the caller's stream)
     uint32_t ps_buffers = 0;        // per-sample result buffers of overlapped frames (RT_PS_BUFFERS,
-                                    // 2-5; 0 = frames in flight + 1)
+                                    // 2-7; 0 = frames in flight + 1)
     int32_t ps_pipeline = -1;       // primary+shadow frames overlap: -1 timed per renderer (auto),
                                     // 0 never, 1 always (RT_PS_PIPELINE)
-    uint32_t ps_depth = 2;          // frames in flight when forced (RT_PS_DEPTH, 2-4)
+    uint32_t ps_depth = 2;          // frames in flight when forced (RT_PS_DEPTH, 2-6)
     float tune_delay_ms = 100.0f;   // GPU time a parameter set runs before its timed choices start
                                     // (RT_TUNE_DELAY_MS): the clocks ramp over ~0.1 s, and choices
                                     // timed on the first frames at low clocks came out wrong
@@ -88,6 +88,10 @@ struct rt_scene {
     size_t scratch_bytes = 0;
     hipStream_t stream = nullptr;
 };
+
+// frames in flight of overlapped primary+shadow frames: up to 6 renderer streams (with the
+// caller's and a communicator's stream, 8 = the bench's GPU_MAX_HW_QUEUES)
+constexpr int kPsMaxDepth = 6;
 
 struct rt_renderer {
     rt_scene *scene = nullptr;
@@ -131,8 +135,8 @@ struct rt_renderer {
     float4 *d_sum = nullptr;        // the running sample sum across batches (serial path)
     // renderer streams: the path tracer's two path streams are 0 and 1; overlapped primary+
     // shadow frames use the first `depth` of them (frames in flight)
-    hipStream_t pt_stream[4] = {};
-    hipEvent_t pt_lv[4] = {};       // a renderer stream's work of this frame is done
+    hipStream_t pt_stream[kPsMaxDepth] = {};
+    hipEvent_t pt_lv[kPsMaxDepth] = {};   // a renderer stream's work of this frame is done
     hipEvent_t pt_fin[3] = {nullptr, nullptr, nullptr};   // the finish that read d_res[b] is done
     bool pt_fin_set[3] = {false, false, false};
     int pt_slot = 0, pt_parity = 0;
@@ -142,20 +146,21 @@ struct rt_renderer {
     // clock ramp of a fresh process cancels -- are timed on the caller's stream (events
     // pev[2g], pev[2g + 1] around group g); the next frame keeps the fastest mode for the
     // parameter set
-    int ps_phase = 0;               // 0 .. 6 kPsGroup - 1 timing frames, 6 kPsGroup decide, -1 decided
+    int ps_phase = 0;               // 0 .. groups x kPsGroup - 1 timing frames, then decide; -1 decided
+    int ps_groups = 0;              // timed groups of this decision (4: serial / 2; 8: serial / 2 / 4 / 6)
     uint32_t ps_use = 0;            // decided: frames in flight (0 = serial)
     uint64_t ps_last = 0;           // r->frames at the last timing frame (any other frame restarts)
     uint32_t ps_prev = 0;           // frames in flight of the previous eligible frame (0 serial)
-    hipEvent_t pev[12] = {};
+    hipEvent_t pev[16] = {};
     hipEvent_t ps_join = nullptr;   // caller's stream -> overlap stream, on a switch to overlapped
-    float ps_ms[6] = {};
+    float ps_ms[8] = {};
     // the overlapped frames' per-sample results, frame n in buffer n % buffers (kernel on
     // renderer stream n % depth): frame n + buffers waits for the finishing pass of frame n only,
     // so a kernel never waits for the finish of a frame still running beside it
-    float4 *ps_res[5] = {};
-    size_t ps_res_bytes[5] = {};
-    hipEvent_t ps_fin[5] = {};
-    bool ps_fin_set[5] = {};
+    float4 *ps_res[kPsMaxDepth + 1] = {};
+    size_t ps_res_bytes[kPsMaxDepth + 1] = {};
+    hipEvent_t ps_fin[kPsMaxDepth + 1] = {};
+    bool ps_fin_set[kPsMaxDepth + 1] = {};
     uint32_t ps_count = 0;
     // tuning gate: the timed choices (camera walk, split order, frames in flight) of a parameter
     // set start once its frames have run tune_delay_ms of GPU time -- an event at its first frame
@@ -655,8 +660,8 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_XCD_ORDER")) s->xcd_order = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_PIPELINE")) s->pt_pipeline = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PS_PIPELINE")) s->ps_pipeline = std::max(-1, std::min(1, std::atoi(e)));
-    if (const char *e = std::getenv("RT_PS_BUFFERS")) s->ps_buffers = (uint32_t)std::max(2, std::min(5, std::atoi(e)));
-    if (const char *e = std::getenv("RT_PS_DEPTH")) s->ps_depth = (uint32_t)std::max(2, std::min(4, std::atoi(e)));
+    if (const char *e = std::getenv("RT_PS_BUFFERS")) s->ps_buffers = (uint32_t)std::max(2, std::min(kPsMaxDepth + 1, std::atoi(e)));
+    if (const char *e = std::getenv("RT_PS_DEPTH")) s->ps_depth = (uint32_t)std::max(2, std::min(kPsMaxDepth, std::atoi(e)));
     if (const char *e = std::getenv("RT_TUNE_DELAY_MS")) s->tune_delay_ms = (float)std::max(0.0, std::atof(e));
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
@@ -754,7 +759,7 @@ constexpr int kPtResBuffers = RT_PT_RES_BUFFERS;   // 2 or 3
 // The renderer's two overlap streams and their ordering events (created once).
 int ensure_pipe_streams(rt_renderer *r) {
     if (r->pt_stream[0]) return RT_OK;
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < kPsMaxDepth; ++k) {
         HIP_TRY(hipStreamCreateWithFlags(&r->pt_stream[k], hipStreamNonBlocking));
         // ordering between streams of this device only: a device-scope release
         HIP_TRY(hipEventCreateWithFlags(&r->pt_lv[k], hipEventDisableTiming | hipEventReleaseToDevice));
@@ -1297,21 +1302,27 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     // frames in flight for this frame: 0 = serial, else 2..4 renderer streams
     uint32_t depth_k = (ps_ok && s->ps_pipeline == 1) ? s->ps_depth : 0u;
     int ps_ev0 = -1, ps_ev1 = -1;   // pev recorded on the caller's stream before / after this frame
-    // 4 frames in flight are a candidate only for frames of a few rounds of resident waves (a
-    // multi-GPU rank's small shard); a throughput-bound frame (TEAPOT-F 1080p, 8 rounds) lost
-    // with them (0.1035 -> 0.114 ms) and the timing only risked picking them
+    // More than 2 frames in flight are candidates only for frames of a few rounds of resident
+    // waves (a multi-GPU rank's small shard, 720p); a throughput-bound frame (TEAPOT-F 1080p, 8
+    // rounds) lost with 4 (0.1035 -> 0.114 ms) and the timing only risked picking them.  Groups
+    // in palindromic order: serial, 2, 4, 6, 6, 4, 2, serial -- or serial, 2, 2, serial.
     const bool deep_ok = F.nunits <= 3u * 4u * 5u * s->num_cus;
+    static const uint32_t kDeep[8] = {0, 2, 4, 6, 6, 4, 2, 0}, kShallow[4] = {0, 2, 2, 0};
     if (ps_ok && s->ps_pipeline < 0 && !gate_open) depth_k = 0;   // timing not started: serial
     if (ps_ok && s->ps_pipeline < 0 && gate_open) {
         constexpr int G = kPsGroup;
-        const uint32_t kGroupDepth[6] = {0, 2, deep_ok ? 4u : 2u, deep_ok ? 4u : 2u, 2, 0};
-        if (r->ps_phase > 0 && r->ps_phase < 6 * G && r->frames != r->ps_last + 1) r->ps_phase = 0;   // interrupted
-        if (r->ps_phase == 6 * G) {
-            HIP_TRY(hipEventSynchronize(r->pev[11]));
-            for (int g = 0; g < 6; ++g) HIP_TRY(hipEventElapsedTime(&r->ps_ms[g], r->pev[2 * g], r->pev[2 * g + 1]));
-            const float t0 = r->ps_ms[0] + r->ps_ms[5], t2 = r->ps_ms[1] + r->ps_ms[4], t4 = r->ps_ms[2] + r->ps_ms[3];
-            if (deep_ok) r->ps_use = (t4 < t2 && t4 < t0) ? 4u : (t2 < t0 ? 2u : 0u);
-            else r->ps_use = 0.25f * (t2 + t4) < 0.5f * t0 ? 2u : 0u;   // groups 1-4 all ran 2 in flight
+        if (r->ps_phase == 0) r->ps_groups = deep_ok ? 8 : 4;
+        const int NG = r->ps_groups;
+        const uint32_t *depths = NG == 8 ? kDeep : kShallow;
+        if (r->ps_phase > 0 && r->ps_phase < NG * G && r->frames != r->ps_last + 1) r->ps_phase = 0;   // interrupted
+        if (r->ps_phase > 0 && r->ps_phase == NG * G) {
+            HIP_TRY(hipEventSynchronize(r->pev[2 * NG - 1]));
+            for (int g = 0; g < NG; ++g) HIP_TRY(hipEventElapsedTime(&r->ps_ms[g], r->pev[2 * g], r->pev[2 * g + 1]));
+            float best = 0.0f;
+            for (int g = 0; g < NG / 2; ++g) {   // group g and its mirror NG - 1 - g ran the same depth
+                const float t = r->ps_ms[g] + r->ps_ms[NG - 1 - g];
+                if (g == 0 || t < best) { best = t; r->ps_use = depths[g]; }
+            }
             r->ps_phase = -1;
         }
         if (r->ps_phase >= 0) {
@@ -1319,12 +1330,13 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
                 if (!r->pev[0])
                     for (auto &e : r->pev) HIP_TRY(hipEventCreate(&e));
                 int rc = ensure_pipe_streams(r);
-                const uint32_t nb = s->ps_buffers ? s->ps_buffers : 5u;
+                const uint32_t maxd = NG == 8 ? 6u : 2u;
+                const uint32_t nb = s->ps_buffers ? s->ps_buffers : maxd + 1u;
                 for (uint32_t k = 0; k < nb && rc == RT_OK; ++k) rc = ensure_ps_res(r, k, ps_bytes);
                 if (rc != RT_OK) return rc;
             }
-            const int g = r->ps_phase / G;   // serial, 2, 4, 4, 2, serial frames in flight
-            depth_k = kGroupDepth[g];
+            const int g = r->ps_phase / G;
+            depth_k = depths[g];
             if (r->ps_phase % G == 0) ps_ev0 = 2 * g;
             if (r->ps_phase % G == G - 1) ps_ev1 = 2 * g + 1;
             r->ps_last = r->frames;
@@ -1678,7 +1690,7 @@ int rt_renderer_destroy(rt_renderer *r) {
     if (r->d_rgb) (void)hipFree(r->d_rgb);
     for (int k = 0; k < 2; ++k)
         if (r->d_pt[k]) (void)hipFree(r->d_pt[k]);
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < kPsMaxDepth; ++k) {
         if (r->pt_stream[k]) (void)hipStreamDestroy(r->pt_stream[k]);
         if (r->pt_lv[k]) (void)hipEventDestroy(r->pt_lv[k]);
     }
@@ -1701,7 +1713,7 @@ int rt_renderer_destroy(rt_renderer *r) {
     for (auto &e : r->gate_ev)
         if (e) (void)hipEventDestroy(e);
     if (r->ps_join) (void)hipEventDestroy(r->ps_join);
-    for (int b = 0; b < 5; ++b) {
+    for (int b = 0; b < kPsMaxDepth + 1; ++b) {
         if (r->ps_res[b]) (void)hipFree(r->ps_res[b]);
         if (r->ps_fin[b]) (void)hipEventDestroy(r->ps_fin[b]);
     }
@@ -1809,17 +1821,34 @@ int rt_renderer_counters(rt_renderer *r, rt_counters *out) {
 int rt_renderer_overlap(const rt_renderer *r, int *state, float ms[4]) {
     if (!r || !state) return fail(RT_ERR_INVALID, "rt_renderer_overlap: null argument");
     int depth = 0;
-    float all[6];
+    float all[8];
     rt_renderer_overlap_depth(r, &depth, all);
     *state = depth < 0 ? -1 : (depth > 1 ? 1 : 0);
-    if (ms) {   // serial, 2 in flight, 2 in flight, serial: the groups of the two-mode decision
-        const int g[4] = {0, 1, 4, 5};
+    if (ms) {   // serial, 2 in flight, 2 in flight, serial
+        const int n = r->ps_groups == 8 ? 8 : 4;
+        const int g[4] = {0, 1, n - 2, n - 1};
         for (int k = 0; k < 4; ++k) ms[k] = all[g[k]];
     }
     return RT_OK;
 }
 
-int rt_renderer_overlap_depth(const rt_renderer *r, int *depth, float ms[6]) {
+int rt_renderer_choices(const rt_renderer *r, int *walk, int *split, float walk_ms[4], float split_ms[4]) {
+    if (!r || !walk || !split) return fail(RT_ERR_INVALID, "rt_renderer_choices: null argument");
+    const rt_scene *s = r->scene;
+    *walk = s->walk == RT_WALK_WAVE ? 1 : s->walk == RT_WALK_LANE ? 0 : (r->tune == kTuneDone ? (r->wave ? 1 : 0) : -1);
+    *split = r->order_state == 2 && r->split_phase < 0 ? (r->use_split ? 1 : 0) : -1;
+    for (int g = 0; g < 4; ++g) {
+        float t = 0.0f;
+        if (walk_ms) {
+            if (r->tune == kTuneDone && s->walk == RT_WALK_AUTO && r->tev[2 * g]) (void)hipEventElapsedTime(&t, r->tev[2 * g], r->tev[2 * g + 1]);
+            walk_ms[g] = t;
+        }
+        if (split_ms) split_ms[g] = (r->split_phase < 0 && r->order_state == 2) ? r->split_ms[g] : 0.0f;
+    }
+    return RT_OK;
+}
+
+int rt_renderer_overlap_depth(const rt_renderer *r, int *depth, float ms[8]) {
     if (!r || !depth) return fail(RT_ERR_INVALID, "rt_renderer_overlap_depth: null argument");
     const int32_t mode = r->scene->ps_pipeline;
     const bool decided = mode < 0 && r->ps_phase == -1;
@@ -1827,7 +1856,7 @@ int rt_renderer_overlap_depth(const rt_renderer *r, int *depth, float ms[6]) {
     else if (mode == 1) *depth = (int)r->scene->ps_depth;
     else *depth = decided ? (r->ps_use ? (int)r->ps_use : 1) : -1;
     if (ms)
-        for (int g = 0; g < 6; ++g) ms[g] = decided ? r->ps_ms[g] : 0.0f;
+        for (int g = 0; g < 8; ++g) ms[g] = (decided && g < r->ps_groups) ? r->ps_ms[g] : 0.0f;
     return RT_OK;
 }
 

@@ -308,11 +308,18 @@ int rt_renderer_counters(rt_renderer *r, rt_counters *out);
  * the first eligible frames); ms (may be NULL) = the serial and 2-in-flight groups' milliseconds
  * (serial, overlapped, overlapped, serial) when decided by timing, else zeros. */
 int rt_renderer_overlap(const rt_renderer *r, int *state, float ms[4]);
-/* The same decision with its depth: *depth = primary+shadow frames in flight (1 serial, 2..4
- * overlapped on that many renderer streams; -1 not decided yet).  RT_PS_PIPELINE=-1 times six
- * groups of eight frames -- serial, 2, 4, 4, 2, serial in flight -- and keeps the fastest;
- * RT_PS_PIPELINE=1 forces RT_PS_DEPTH (default 2).  ms (may be NULL) = the six groups' ms. */
-int rt_renderer_overlap_depth(const rt_renderer *r, int *depth, float ms[6]);
+/* The same decision with its depth: *depth = primary+shadow frames in flight (1 serial, 2..6
+ * overlapped on that many renderer streams; -1 not decided yet).  RT_PS_PIPELINE=-1 times groups
+ * of eight frames in palindromic order -- serial, 2, 4, 6, 6, 4, 2, serial in flight for frames
+ * of at most ~3 rounds of resident waves, serial, 2, 2, serial otherwise -- and keeps the
+ * fastest; RT_PS_PIPELINE=1 forces RT_PS_DEPTH (default 2).  ms (may be NULL) = the groups' ms
+ * (8 entries; unused ones 0). */
+int rt_renderer_overlap_depth(const rt_renderer *r, int *depth, float ms[8]);
+/* The renderer's other timed choices for its current parameter set (diagnostics): *walk = the
+ * camera-ray walk of primary+shadow frames (0 lane, 1 wave, -1 not decided); *split = the
+ * half-tile split order of its costliest tiles (1 on, 0 off, -1 not decided / not applicable);
+ * walk_ms / split_ms (may be NULL) = the four timed groups (A, B, B, A) in ms. */
+int rt_renderer_choices(const rt_renderer *r, int *walk, int *split, float walk_ms[4], float split_ms[4]);
 /* The measured cost map behind the longest-tile-first order of the renderer's current parameter
  * set (camera, size, spp, depth, mode, shard): costs[i] = wave cycles (s_memtime ticks) of
  * local tile i, recorded on one frame; *n_out = its tile count (0 until recorded: from the 2nd

@@ -45,7 +45,7 @@ def time_share(scene, a, spp, frames, render):
     c1 = r.counters()
     ms = ev[0].elapsed_time(ev[1]) / frames
     rays = sum(c1[k] - c0[k] for k in ("primary", "shadow", "bounce")) / frames
-    out = {"ms": round(ms, 4), "mrays": round(rays / 1e6, 3), "in_flight": r.overlap_depth()[0]}
+    out = {"ms": round(ms, 4), "mrays": round(rays / 1e6, 3), "in_flight": r.overlap_depth()[0], "choices": r.choices()}
     cost = r.tile_costs().astype(np.float64)
     if cost.size:
         out["tile_cycles_max"] = int(cost.max())

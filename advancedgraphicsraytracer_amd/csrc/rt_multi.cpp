@@ -140,6 +140,7 @@ struct rt_comm {
     uint64_t deal_key = 0;                 // parameter set the balanced deal belongs to
     uint32_t key_calls = 0;                // frames of that parameter set so far
     bool deal_on = false;
+    bool deal_moot = false;                // no costs measured (path-traced frames): keep interleaving
     uint32_t *d_setup = nullptr;           // staging of the exchange
     // RT_MULTI_TIMING: per frame (render start, render end, gather end) events, summed by rt_comm_timing
     std::vector<std::array<hipEvent_t, 3>> tev;
@@ -294,12 +295,17 @@ int exchange_deal(rt_comm *c, rt_renderer *r) {
             }
             complete = complete && (any || il.count(k) == 0);
         }
+        // without measured costs (path-traced frames record none) equal-count regions measured
+        // worse than interleaving (CFG5-sub 1/4 shards 3.36 vs 2.54 ms): keep the interleaved deal
         Deal &d = c->balanced;
-        d.tiles.assign(c->ntiles, 0u);
-        d.off.assign((size_t)c->world + 1, 0u);
-        if ((rc = rt_tile_deal(c->W, c->H, complete ? global.data() : nullptr, (uint32_t)c->world, d.tiles.data(),
-                               d.off.data())) != RT_OK)
-            return rc;
+        if (complete) {
+            d.tiles.assign(c->ntiles, 0u);
+            d.off.assign((size_t)c->world + 1, 0u);
+            if ((rc = rt_tile_deal(c->W, c->H, global.data(), (uint32_t)c->world, d.tiles.data(), d.off.data())) != RT_OK)
+                return rc;
+        } else {
+            d = c->interleaved;
+        }
         if (c->world > 1) {
             std::vector<uint32_t> msg(d.off);
             msg.insert(msg.end(), d.tiles.begin(), d.tiles.end());
@@ -323,6 +329,7 @@ int exchange_deal(rt_comm *c, rt_renderer *r) {
         c->balanced.tiles.assign(msg.begin() + c->world + 1, msg.end());
     }
     c->deal_on = true;
+    c->deal_moot = c->balanced.tiles == c->interleaved.tiles && c->balanced.off == c->interleaved.off;
     c->deal_version += 1;
     return RT_OK;
 }
@@ -539,7 +546,7 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
     if ((flags & RT_MULTI_BALANCED) && !c->deal_on && c->key_calls >= kDealAfter && (rc = exchange_deal(c, r)) != RT_OK)
         return rc;
     c->key_calls += 1;
-    const bool use_balanced = (flags & RT_MULTI_BALANCED) && c->deal_on;
+    const bool use_balanced = (flags & RT_MULTI_BALANCED) && c->deal_on && !c->deal_moot;
     const Deal &deal = use_balanced ? c->balanced : c->interleaved;
     const int deal_id = use_balanced ? 1 : 0;
     if (c->world > 1 && c->last_deal >= 0 && (c->last_deal != deal_id || (deal_id == 1 && c->last_version != c->deal_version))) {

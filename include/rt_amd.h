@@ -288,9 +288,11 @@ int rt_comm_destroy(rt_comm *c);
 #define RT_MULTI_TIMING 2u
 /* RT_MULTI_BALANCED: from the 7th frame of a parameter set (camera, size, spp, depth, mode) on,
  * the ranks render the cost-balanced compact deal of rt_tile_deal instead of t % world: built
- * once per parameter set from every rank's measured tile costs (rt_renderer_tile_costs; equal
- * costs where none were measured) in one exchange -- the costs to rank 0, the deal back to all.
- * Frames are identical under any deal; every rank must pass the same flags. */
+ * once per parameter set from every rank's measured tile costs (rt_renderer_tile_costs; where a
+ * rank measured none -- path-traced frames -- the interleaved deal stays) in one exchange: the
+ * costs to rank 0, the deal back to all.  When tiles change owner the ranks' accumulators are
+ * merged first, so accumulation goes on exactly.  Frames are identical under any deal; every
+ * rank must pass the same flags. */
 #define RT_MULTI_BALANCED 4u
 int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, const rt_frame_params *p,
                           uint32_t *rgb8_dev, uint32_t flags, void *stream);

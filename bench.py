@@ -102,6 +102,8 @@ def parse():
                     help="untimed frames before the warm-up steps until this much wall time has passed: the "
                          "GPU clocks ramp up over ~0.1 s, and 5 warm-up frames are only ~0.5 ms of work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-companion", action="store_true", help="skip the 1280x720 companion run (profiling runs: "
+                    "its frames would share the frame kernel's name in the kernel trace)")
     ap.add_argument("--per-step-events", action="store_true", help="HIP event pair around every launch at N = 1 too")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the all-cores CPU baseline sample")
     ap.add_argument("--summary", default=rl.SUMMARY, help="rocprofv3 PMC / kernel-trace summary (tools/roofline.py)")
@@ -346,7 +348,7 @@ def main():
     wall = t_max.item()
     overlap = rend.overlap()
     companion = None
-    if world == 1 and args.depth == 1 and (W, H) == (1920, 1080):   # the metric's other frame size
+    if world == 1 and args.depth == 1 and (W, H) == (1920, 1080) and not args.no_companion:   # the metric's other frame size
         companion = companion_rate(scene, 1280, 720, spp, args.depth, stream, device)
 
     if rank == 0:

@@ -164,6 +164,7 @@ def lib():
         "rt_renderer_read_accumulator": ([vp, fp], C.c_int),
         "rt_renderer_overlap": ([vp, C.POINTER(C.c_int), fp], C.c_int),
         "rt_renderer_overlap_depth": ([vp, C.POINTER(C.c_int), fp], C.c_int),
+        "rt_renderer_device_bytes": ([vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)], C.c_int),
         "rt_renderer_tile_costs": ([vp, C.POINTER(u32), u32, C.POINTER(u32)], C.c_int),
         "rt_renderer_choices": ([vp, C.POINTER(C.c_int), C.POINTER(C.c_int), fp, fp], C.c_int),
         "rt_renderer_stream": ([vp, C.POINTER(vp)], C.c_int),
@@ -720,6 +721,12 @@ class Renderer:
         ms = np.zeros(8, np.float32)
         _check(self.L.rt_renderer_overlap_depth(self.h, C.byref(d), _fptr(ms)))
         return d.value, [round(float(x), 4) for x in ms]
+
+    def device_bytes(self):
+        """(bytes of device memory the renderer holds, overlapped-frame result buffers allocated)."""
+        b, n = C.c_uint64(), C.c_uint32()
+        _check(self.L.rt_renderer_device_bytes(self.h, C.byref(b), C.byref(n)))
+        return b.value, n.value
 
     def choices(self):
         """Timed choices of the current parameter set: {walk: 0 lane / 1 wave / -1, split: 1 / 0 / -1,

@@ -141,11 +141,11 @@ struct rt_renderer {
     bool pt_fin_set[3] = {false, false, false};
     int pt_slot = 0, pt_parity = 0;
     bool pt_serial_last = false;    // the last path-traced frame ran the serial path
-    // overlapped primary+shadow frames (launch_render): with RT_PS_PIPELINE auto, six groups of
-    // kPsGroup eligible frames back to back -- serial, 2 in flight, 4, 4, 2, serial, so that the
-    // clock ramp of a fresh process cancels -- are timed on the caller's stream (events
-    // pev[2g], pev[2g + 1] around group g); the next frame keeps the fastest mode for the
-    // parameter set
+    // overlapped primary+shadow frames (launch_render): with RT_PS_PIPELINE auto, eight groups
+    // of kPsGroup eligible frames back to back -- serial, 2 in flight, 4, 6, 6, 4, 2, serial (or
+    // four: serial, 2, 2, serial), so that a clock drift cancels -- are timed on the caller's
+    // stream (events pev[2g], pev[2g + 1] around group g); the next frame keeps the fastest mode
+    // for the parameter set, and the result buffers it does not use are freed
     int ps_phase = 0;               // 0 .. groups x kPsGroup - 1 timing frames, then decide; -1 decided
     int ps_groups = 0;              // timed groups of this decision (4: serial / 2; 8: serial / 2 / 4 / 6)
     uint32_t ps_use = 0;            // decided: frames in flight (0 = serial)
@@ -1290,16 +1290,16 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     // the finishing pass's extra 66 MB of sample traffic is not hidden there), and only
     // when the caller submits frames back to back.  A small frame -- a multi-GPU rank's 1/N
     // shard, about one round of resident waves -- is one latency chain long, and more frames
-    // in flight keep filling its idle issue slots: up to 4 renderer streams (round 3).  So by
-    // default each renderer times serial, 2 and 4 frames in flight on its own frames and keeps
-    // the fastest (RT_PS_PIPELINE: -1 auto, 0 off, 1 on with RT_PS_DEPTH frames in flight).
+    // in flight keep filling its idle issue slots: up to 6 renderer streams (round 3).  So by
+    // default each renderer times serial, 2, 4 and 6 frames in flight on its own frames and
+    // keeps the fastest (RT_PS_PIPELINE: -1 auto, 0 off, 1 on with RT_PS_DEPTH frames in flight).
     const uint64_t ps_bytes = (uint64_t)p->spp * F.ntiles_local * 64u * 16u;
     // (sample-split frames -- a multi-GPU rank's shard at spp N -- store their samples anyway;
     // overlapped, they go to the result buffers instead of d_samples)
     const bool ps_ok = s->ps_pipeline != 0 && mode == RT_MODE_PATH && md == 1 && lds_kind == 0 &&
                        split_ev0 < 0 && split_ev1 < 0 && r->split_phase < 0 && !F.tile_cost && !walk_pending &&
                        ps_bytes <= (2ull << 30);
-    // frames in flight for this frame: 0 = serial, else 2..4 renderer streams
+    // frames in flight for this frame: 0 = serial, else 2..6 renderer streams
     uint32_t depth_k = (ps_ok && s->ps_pipeline == 1) ? s->ps_depth : 0u;
     int ps_ev0 = -1, ps_ev1 = -1;   // pev recorded on the caller's stream before / after this frame
     // More than 2 frames in flight are candidates only for frames of a few rounds of resident
@@ -1324,6 +1324,15 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
                 if (g == 0 || t < best) { best = t; r->ps_use = depths[g]; }
             }
             r->ps_phase = -1;
+            // every timed frame's finishing pass preceded pev[2 NG - 1]: no buffer is in use, and
+            // the ones the chosen depth never touches are released (a 1080p spp-1 buffer is 33 MB)
+            const uint32_t keep = r->ps_use == 0 ? 0u : (s->ps_buffers ? s->ps_buffers : r->ps_use + 1u);
+            for (uint32_t b = keep; b <= (uint32_t)kPsMaxDepth; ++b) {
+                if (r->ps_res[b]) HIP_TRY(hipFree(r->ps_res[b]));
+                r->ps_res[b] = nullptr;
+                r->ps_res_bytes[b] = 0;
+                r->ps_fin_set[b] = false;
+            }
         }
         if (r->ps_phase >= 0) {
             if (r->ps_phase == 0) {   // streams, events and every result buffer before the timing
@@ -1857,6 +1866,28 @@ int rt_renderer_overlap_depth(const rt_renderer *r, int *depth, float ms[8]) {
     else *depth = decided ? (r->ps_use ? (int)r->ps_use : 1) : -1;
     if (ms)
         for (int g = 0; g < 8; ++g) ms[g] = (decided && g < r->ps_groups) ? r->ps_ms[g] : 0.0f;
+    return RT_OK;
+}
+
+int rt_renderer_device_bytes(const rt_renderer *r, uint64_t *bytes, uint32_t *ps_buffers) {
+    if (!r || !bytes) return fail(RT_ERR_INVALID, "rt_renderer_device_bytes: null argument");
+    const uint64_t pix = (uint64_t)r->W * r->H;
+    const uint64_t tiles = (uint64_t)((r->W + 7) / 8) * ((r->H + 7) / 8);
+    uint64_t b = 16u * pix + kCounterSlots * 8u * sizeof(unsigned long long);   // accumulator, counters
+    if (r->d_rgb) b += 4u * pix;
+    for (int k = 0; k < 2; ++k) b += r->pt_bytes[k];
+    for (size_t k : r->res_bytes) b += k;
+    if (r->d_sum) b += tiles * 64u * sizeof(float4);
+    b += r->samples_bytes;
+    b += 5u * (uint64_t)r->order_n * sizeof(uint32_t);   // plain + split order, two cost maps
+    b += (r->d_map ? r->map_cap : 0) * sizeof(uint32_t) + (r->d_where ? r->where_cap : 0) * sizeof(uint32_t);
+    uint32_t nps = 0;
+    for (int k = 0; k <= kPsMaxDepth; ++k) {
+        b += r->ps_res_bytes[k];
+        nps += r->ps_res[k] != nullptr;
+    }
+    *bytes = b;
+    if (ps_buffers) *ps_buffers = nps;
     return RT_OK;
 }
 

@@ -201,7 +201,7 @@ def companion_rate(scene, W, H, spp, depth, stream, device, warm_s=0.4, frames=3
         wall = time.perf_counter() - t0
     c1 = r.counters()
     rays = sum(c1[k] - c0[k] for k in ("primary", "shadow", "bounce"))
-    return {"width": W, "height": H, "spp": spp, "depth": depth, "frames": frames, "overlapped": r.overlap()[0],
+    return {"width": W, "height": H, "spp": spp, "depth": depth, "frames": frames, "overlapped": r.overlap()[0], "in_flight": r.overlap_depth()[0],
             "ms_per_frame": round(wall / frames * 1e3, 4), "frame_ms_events": round(e0.elapsed_time(e1) / frames, 4),
             "mrays_s": round(rays / wall / 1e6, 3), "fps": round(frames / wall, 3)}
 
@@ -347,6 +347,7 @@ def main():
     tot_rays, tot_primary, tot_shadow, tot_bounce = local_rays.tolist()
     wall = t_max.item()
     overlap = rend.overlap()
+    in_flight = rend.overlap_depth()
     companion = None
     if world == 1 and args.depth == 1 and (W, H) == (1920, 1080) and not args.no_companion:   # the metric's other frame size
         companion = companion_rate(scene, 1280, 720, spp, args.depth, stream, device)
@@ -400,8 +401,10 @@ def main():
             "roofline": roof,
         }
         if args.depth == 1:   # RT_PS_PIPELINE: serial or overlapped primary+shadow frames (rank 0)
-            line["overlapped_frames"] = {"state": overlap[0], "timed_groups_ms": overlap[1],
-                                         "groups": "serial, overlapped, overlapped, serial (8 frames each)"}
+            groups = [g for g in in_flight[1] if g > 0]
+            line["overlapped_frames"] = {"state": overlap[0], "in_flight": in_flight[0], "timed_groups_ms": groups,
+                                         "groups": ("frames in flight serial, 2, 4, 6, 6, 4, 2, serial" if len(groups) == 8
+                                                    else "frames in flight serial, 2, 2, serial") + " (8 frames each)"}
         if multi:
             line["multi_gpu"] = multi
         if companion:

@@ -317,6 +317,11 @@ int rt_renderer_overlap(const rt_renderer *r, int *state, float ms[4]);
  * fastest; RT_PS_PIPELINE=1 forces RT_PS_DEPTH (default 2).  ms (may be NULL) = the groups' ms
  * (8 entries; unused ones 0). */
 int rt_renderer_overlap_depth(const rt_renderer *r, int *depth, float ms[8]);
+/* Device memory the renderer holds right now (diagnostics; INTEGRATION.md "Device memory per
+ * renderer"): *bytes = accumulator, counters, RGB8, path-state slots, result and sample buffers,
+ * tile orders and deal maps; *ps_buffers (may be NULL) = overlapped-frame result buffers allocated
+ * (up to 7 while the frames-in-flight choice is timed, depth + 1 or 0 after it). */
+int rt_renderer_device_bytes(const rt_renderer *r, uint64_t *bytes, uint32_t *ps_buffers);
 /* The renderer's other timed choices for its current parameter set (diagnostics): *walk = the
  * camera-ray walk of primary+shadow frames (0 lane, 1 wave, -1 not decided); *split = the
  * half-tile split order of its costliest tiles (1 on, 0 off, -1 not decided / not applicable);

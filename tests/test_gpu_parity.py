@@ -539,11 +539,12 @@ def test_pipelined_batches_equal_serial(rt, torch, monkeypatch, recipe, W, H, me
 def test_overlapped_primary_shadow_frames_equal_serial(rt, torch, monkeypatch, recipe, W, H, shards, mode, depth):
     """Primary+shadow frames past the tuning frames (camera walk, tile-cost order, split order)
     run their frame kernel on the renderer's overlap streams -- `depth` frames in flight -- and
-    accumulate in a finishing pass (RT_PS_PIPELINE=1; -1 = the default, which times serial, 2
-    and 4 frames in flight and keeps the fastest) -- against the serial frame kernel on the
+    accumulate in a finishing pass (RT_PS_PIPELINE=1; -1 = the default, which times serial, 2,
+    4 and 6 frames in flight and keeps the fastest) -- against the serial frame kernel on the
     caller's stream: 126 frames back to back with spp 2 frames, a path-traced frame and a reset
     interleaved, whole frames or shard 1 of `shards` (packed tiles); every frame, the
-    accumulator and the ray counters bit for bit."""
+    accumulator and the ray counters bit for bit.  After the choice a renderer holds exactly the
+    result buffers its depth uses (depth + 1; none when serial)."""
     monkeypatch.setenv("RT_PS_PIPELINE", "0")
     s0 = rt.Scene.recipe(recipe)
     monkeypatch.setenv("RT_PS_PIPELINE", mode)
@@ -554,7 +555,7 @@ def test_overlapped_primary_shadow_frames_equal_serial(rt, torch, monkeypatch, r
                                     (1, 1, False)]
     cap = r0.shard_capacity(shards)
     st = torch.cuda.Stream()
-    outs, states = [], []
+    outs, states, nbuf = [], [], []
     with torch.cuda.stream(st):
         for r in (r0, r1):
             frames = []
@@ -568,11 +569,13 @@ def test_overlapped_primary_shadow_frames_equal_serial(rt, torch, monkeypatch, r
                 frames.append(o)
                 if f == 119:
                     states.append(r.overlap_depth()[0])
+                    nbuf.append(r.device_bytes()[1])
             outs.append(frames)
     torch.cuda.synchronize()
     # frames in flight each renderer runs after its 120 primary+shadow frames (walk, split order and
     # frames in flight timed: ~85 frames)
     assert states[0] == 1 and (states[1] == depth if mode == "1" else states[1] in (1, 2, 4, 6)), states
+    assert nbuf == [0, 0 if states[1] == 1 else states[1] + 1], (states, nbuf)
     for f in range(len(plan)):
         a, b = outs[0][f].cpu().numpy(), outs[1][f].cpu().numpy()
         assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"

@@ -1,5 +1,5 @@
 """The bench line's roofline is reproducible from the tracked rocprofv3 outputs: re-parsing
-profiles/r02/cfgN (kernel-trace stats + PMC passes) gives the committed summary, and every
+profiles/r0N/cfgN (kernel-trace stats or per-launch trace + PMC passes) gives the committed summary, and every
 config's binding-resource fraction is a fraction (<= 1)."""
 import os
 import sys
@@ -21,7 +21,7 @@ def test_summary_recomputes_from_tracked_csvs(key):
     rec = summary[key]
     dirs = [os.path.join(ROOT, d) for d in rec["sources"]]
     assert all(os.path.isdir(d) for d in dirs), rec["sources"]
-    again = rl.summarize(key, KERNELS[key], dirs)
+    again = rl.summarize(key, KERNELS[key], dirs, tail=rec.get("tail"))
     assert again["counters"] == pytest.approx(rec["counters"])
     assert again["trace_avg_ns"] == pytest.approx(rec["trace_avg_ns"])
     r = rl.roofline(again)

@@ -47,7 +47,7 @@ for s in "$@"; do
                 step pmc_c${c}_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pc$c/write -o pmc --output-format csv -- $b
                 step pmc_c${c}_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d gpurun_out/pc$c/sq -o pmc --output-format csv -- $b
                 step pmc_c${c}_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pc$c/tcc -o pmc --output-format csv -- $b
-                step sum_c$c 60 python tools/roofline.py summarize cfg$c "$k" gpurun_out/pc$c/trace gpurun_out/pc$c/fetch gpurun_out/pc$c/write gpurun_out/pc$c/sq gpurun_out/pc$c/tcc --out gpurun_out/pmc_summary.json
+                step sum_c$c 60 python tools/roofline.py summarize cfg$c "$k" gpurun_out/pc$c/trace gpurun_out/pc$c/fetch gpurun_out/pc$c/write gpurun_out/pc$c/sq gpurun_out/pc$c/tcc --tail 0.5 --out gpurun_out/pmc_summary.json
             done
             unset RT_PS_PIPELINE ;;
         prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 100 --warmup 5 --no-cpu-baseline ;;

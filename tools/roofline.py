@@ -19,7 +19,7 @@ Beside it: HBM bytes per launch (FETCH_SIZE x 2 -- gfx950 counts half of a wide 
 (renamed algorithmic_gbs: node / triangle bytes mostly served by L1/L2, never a fraction).
 
 usage:
-  roofline.py summarize KEY KERNEL_SUBSTR DIR [DIR ...] [--out profiles/pmc_summary.json]
+  roofline.py summarize KEY KERNEL_SUBSTR DIR [DIR ...] [--out profiles/pmc_summary.json] [--tail 0.5]
       parse a workload's rocprofv3 runs (kernel-trace stats + PMC passes) under DIRs
   roofline.py show [--summary profiles/pmc_summary.json]
       print every workload's roofline fields, recomputed from the summary
@@ -50,19 +50,29 @@ def _rows(dirs, pattern):
                 yield from csv.DictReader(fh)
 
 
-def summarize(key, kernel, dirs):
+def summarize(key, kernel, dirs, tail=None):
     """Per-launch means of every counter found for kernels whose name contains `kernel`,
-    and the kernel-trace average duration (rocprofv3 --stats)."""
-    sums, counts = {}, {}
+    and the kernel-trace average duration (rocprofv3 --stats).  tail (0 < tail <= 1): average
+    only the last `tail` fraction of each counter's dispatches (by Dispatch_Id) and, when the
+    per-launch kernel trace (*kernel_trace.csv) is there, of the launches -- the steady state
+    after the renderer's untimed ramp and tuning frames (the bench's timed region)."""
+    per = {}
     for row in _rows(dirs, "*counter_collection.csv"):
         if kernel not in row.get("Kernel_Name", ""):
             continue
         name = row["Counter_Name"]
         if name in COUNTERS:
-            sums[name] = sums.get(name, 0.0) + float(row["Counter_Value"])
-            counts[name] = counts.get(name, 0) + 1
-    rec = {"kernel": kernel, "counters": {k: sums[k] / counts[k] for k in sums},
-           "dispatches": {k: counts[k] for k in counts}}
+            per.setdefault(name, []).append((int(row.get("Dispatch_Id") or 0), float(row["Counter_Value"])))
+
+    def keep(vals):
+        if not tail:
+            return vals
+        vals = sorted(vals)
+        return vals[len(vals) - max(1, int(round(len(vals) * tail))):]
+
+    kept = {k: keep(v) for k, v in per.items()}
+    rec = {"kernel": kernel, "counters": {k: sum(x for _, x in v) / len(v) for k, v in kept.items()},
+           "dispatches": {k: len(v) for k, v in kept.items()}}
     for row in _rows(dirs, "*kernel_stats.csv"):
         if kernel in row.get("Name", ""):
             rec["trace_avg_ns"] = float(row["AverageNs"])
@@ -70,6 +80,15 @@ def summarize(key, kernel, dirs):
             rec["trace_total_ns"] = float(row["TotalDurationNs"])
             rec["trace_kernel_name"] = row["Name"]
             break
+    if tail:
+        rec["tail"] = tail
+        launches = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                    for r in _rows(dirs, "*kernel_trace.csv") if kernel in r.get("Kernel_Name", "")]
+        if launches:
+            d = [x for _, x in keep(launches)]
+            rec["trace_all_avg_ns"] = rec.get("trace_avg_ns")
+            rec["trace_avg_ns"] = sum(d) / len(d)
+            rec["trace_steady_launches"] = len(d)
     # share of the kernel in the frame: every kernel's total time in the same trace
     tot = sum(float(r["TotalDurationNs"]) for r in _rows(dirs, "*kernel_stats.csv")
               if not r["Name"].startswith("__amd") and "Functor" not in r["Name"])
@@ -136,12 +155,13 @@ def main():
     a.add_argument("kernel")
     a.add_argument("dirs", nargs="+")
     a.add_argument("--out", default=SUMMARY)
+    a.add_argument("--tail", type=float, default=None, help="average the last fraction of the dispatches only")
     b = sub.add_parser("show")
     b.add_argument("--summary", default=SUMMARY)
     args = ap.parse_args()
     if args.cmd == "summarize":
         data = load(args.out)
-        data[args.key] = summarize(args.key, args.kernel, args.dirs)
+        data[args.key] = summarize(args.key, args.kernel, args.dirs, tail=args.tail)
         os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
         with open(args.out, "w") as f:
             json.dump(data, f, indent=1, sort_keys=True)

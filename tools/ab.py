@@ -4,7 +4,7 @@
 between builds; the per-build median and min of the per-frame kernel time are printed.
 
 usage: ab.py LIB[@mode=M,depth=D] [...] [--scene teapotF] [--w 1920] [--h 1080] [--spp 1]
-             [--depth 1] [--rounds 7] [--frames 20] [--check]
+             [--depth 1] [--rounds 7] [--frames 20] [--check] [--ramp-seconds 1]
 A LIB may carry its own integrator mode (0 path, 1 Whitted, 2 packet) and depth, so one
 build can be timed against itself in another mode.
 --check compares every entry's RGB8 frame with the first entry's (bit-exact).
@@ -14,6 +14,7 @@ import ctypes as C
 import json
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -46,6 +47,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--ramp-seconds", type=float, default=1.0, help="untimed frames of every build first (clock ramp)")
     a = ap.parse_args()
     builds = []      # (key, spec, lib, scene, renderer, camera, out, mode, depth) per entry
     loaded = {}
@@ -74,12 +76,23 @@ def main():
                 del os.environ[k]
     times = [[] for _ in builds]
     frame = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < a.ramp_seconds:
+        for key, p, L, sc, r, cam, out, mode, depth in builds:
+            fp = rt.FrameParams(a.w, a.h, a.spp, depth, frame, mode, 0)
+            L.rt_render_frame(r, C.byref(cam), C.byref(fp), C.c_void_p(out.data_ptr()), None)
+        torch.cuda.synchronize()
+        frame += 1
     for rnd in range(a.rounds):
         for i, (key, p, L, sc, r, cam, out, mode, depth) in enumerate(builds):
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             # warm + timed frames on the default stream
             fp = rt.FrameParams(a.w, a.h, a.spp, depth, frame, mode, 0)
             L.rt_render_frame(r, C.byref(cam), C.byref(fp), C.c_void_p(out.data_ptr()), None)
+            # idle GPU before the first event: pipelined path-traced frames start their levels on
+            # the renderer's streams without waiting for the caller's stream, so an event recorded
+            # behind a running frame would miss the next frame's early work
+            torch.cuda.synchronize()
             ev[0].record()
             for k in range(a.frames):
                 fp = rt.FrameParams(a.w, a.h, a.spp, depth, frame + 1 + k, mode, 0)

@@ -32,9 +32,9 @@ for s in "$@"; do
             step sortab_c5 600 env GPU_MAX_HW_QUEUES=8 python tools/knob_ab.py --scene cfg5 --spp 16 --depth 10 --var RT_PT_SORT=0 --var RT_PT_SORT=1 --var RT_PT_SORT=3 --check --out gpurun_out/knob_ab.jsonl
             step sortab_c3 600 env GPU_MAX_HW_QUEUES=8 python tools/knob_ab.py --scene cfg3 --spp 4 --depth 4 --var RT_PT_SORT=0 --var RT_PT_SORT=1 --var RT_PT_SORT=3 --check --out gpurun_out/knob_ab.jsonl ;;
         benchcfg)
-            step bench_cfg3 300 python bench.py --config 3 --steps 10 --warmup 2 --no-cpu-baseline
+            step bench_cfg3 300 python bench.py --config 3 --steps 30 --warmup 3 --no-cpu-baseline
             step bench_cfg4 300 python bench.py --config 4 --steps 30 --warmup 5 --no-cpu-baseline
-            step bench_cfg5 300 python bench.py --config 5 --steps 10 --warmup 2 --no-cpu-baseline ;;
+            step bench_cfg5 300 python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline ;;
         profcfg)   # kernel trace + PMC passes of every config's bench run, summarised by tools/roofline.py
             # serial frames (RT_PS_PIPELINE=0): overlapped kernels share the CUs, so their trace
             # durations would not be one kernel's; no 720p companion run (same kernel name)

@@ -73,6 +73,7 @@ struct rt_scene {
     uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per slot (two when pipelined): 12 GB
                                               // of the 288 GB HBM holds all 16 spp of a 1080p depth-10 frame
     bool pt_pipeline = true;        // sample batches alternate path-state slots and streams
+    uint32_t pt_slots = 4;          // path-state slots / streams of pipelined frames (RT_PT_SLOTS, 2-4)
                                     // (RT_PT_PIPELINE=0: one slot, the caller's stream)
     uint32_t ps_buffers = 0;        // per-sample result buffers of overlapped frames (RT_PS_BUFFERS,
                                     // 2-7; 0 = frames in flight + 1)
@@ -92,6 +93,7 @@ struct rt_scene {
 // frames in flight of overlapped primary+shadow frames: up to 6 renderer streams (with the
 // caller's and a communicator's stream, 8 = the bench's GPU_MAX_HW_QUEUES)
 constexpr int kPsMaxDepth = 6;
+constexpr int kPtMaxSlots = 4;    // path-state slots of pipelined path-traced frames (RT_PT_SLOTS; <= kPsMaxDepth streams)
 
 struct rt_renderer {
     rt_scene *scene = nullptr;
@@ -126,20 +128,22 @@ struct rt_renderer {
     // buffer (two, by frame parity); one finishing pass per frame on the caller's stream sums
     // it in sample order after every batch's levels (accumulator, RGB8).  d_pt[0] / the
     // caller's stream alone when pipelining is off or the results do not fit.
-    void *d_pt[2] = {nullptr, nullptr};
-    size_t pt_bytes[2] = {0, 0};
-    // [sample][pixel] radiance of a frame, frame n in buffer n % kPtResBuffers: frame n + 3's
-    // batches wait for frame n's finishing pass only (see kPtResBuffers)
-    float4 *d_res[3] = {nullptr, nullptr, nullptr};
-    size_t res_bytes[3] = {0, 0, 0};
+    void *d_pt[kPtMaxSlots] = {};
+    size_t pt_bytes[kPtMaxSlots] = {};
+    // [sample][pixel] radiance of a frame, frame n in buffer n % (slots + 1): frame n + slots + 1's
+    // batches wait for frame n's finishing pass only (see launch_pt_frame)
+    float4 *d_res[kPtMaxSlots + 1] = {};
+    size_t res_bytes[kPtMaxSlots + 1] = {};
     float4 *d_sum = nullptr;        // the running sample sum across batches (serial path)
     // renderer streams: the path tracer's two path streams are 0 and 1; overlapped primary+
     // shadow frames use the first `depth` of them (frames in flight)
     hipStream_t pt_stream[kPsMaxDepth] = {};
     hipEvent_t pt_lv[kPsMaxDepth] = {};   // a renderer stream's work of this frame is done
-    hipEvent_t pt_fin[3] = {nullptr, nullptr, nullptr};   // the finish that read d_res[b] is done
-    bool pt_fin_set[3] = {false, false, false};
+    hipEvent_t pt_fin[kPtMaxSlots + 1] = {};   // the finish that read d_res[b] is done
+    bool pt_fin_set[kPtMaxSlots + 1] = {};
     int pt_slot = 0, pt_parity = 0;
+    uint32_t pt_nslots = 0;         // slots in use, decided for path state of up to pt_need bytes
+    size_t pt_need = 0;
     bool pt_serial_last = false;    // the last path-traced frame ran the serial path
     // overlapped primary+shadow frames (launch_render): with RT_PS_PIPELINE auto, eight groups
     // of kPsGroup eligible frames back to back -- serial, 2 in flight, 4, 6, 6, 4, 2, serial (or
@@ -659,6 +663,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     s->xcd_order = (size_t)s->bvh.nodes_used * 32u + (size_t)n * 48u > (4u << 20);
     if (const char *e = std::getenv("RT_XCD_ORDER")) s->xcd_order = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_PIPELINE")) s->pt_pipeline = std::atoi(e) != 0;
+    if (const char *e = std::getenv("RT_PT_SLOTS")) s->pt_slots = (uint32_t)std::max(2, std::min((int)kPtMaxSlots, std::atoi(e)));
     if (const char *e = std::getenv("RT_PS_PIPELINE")) s->ps_pipeline = std::max(-1, std::min(1, std::atoi(e)));
     if (const char *e = std::getenv("RT_PS_BUFFERS")) s->ps_buffers = (uint32_t)std::max(2, std::min(kPsMaxDepth + 1, std::atoi(e)));
     if (const char *e = std::getenv("RT_PS_DEPTH")) s->ps_depth = (uint32_t)std::max(2, std::min(kPsMaxDepth, std::atoi(e)));
@@ -748,13 +753,10 @@ int set_tile_map(rt_renderer *r, const uint32_t *tiles, uint32_t n, uint32_t nti
 }
 
 
-// Per-sample result buffers of pipelined path-traced frames: with two (by frame parity), frame
-// n + 2's batches waited for frame n's finishing pass, which itself follows frame n + 1's levels
-// on the caller's stream; three let a frame start behind the finish of the frame before last.
-#ifndef RT_PT_RES_BUFFERS
-#define RT_PT_RES_BUFFERS 3
-#endif
-constexpr int kPtResBuffers = RT_PT_RES_BUFFERS;   // 2 or 3
+// Per-sample result buffers of pipelined path-traced frames: with two slots and two buffers
+// (by frame parity), frame n + 2's batches waited for frame n's finishing pass, which itself
+// follows frame n + 1's levels on the caller's stream; slots + 1 buffers let a frame start
+// behind the finish of the frame `slots` back.
 
 // The renderer's two overlap streams and their ordering events (created once).
 int ensure_pipe_streams(rt_renderer *r) {
@@ -764,7 +766,7 @@ int ensure_pipe_streams(rt_renderer *r) {
         // ordering between streams of this device only: a device-scope release
         HIP_TRY(hipEventCreateWithFlags(&r->pt_lv[k], hipEventDisableTiming | hipEventReleaseToDevice));
     }
-    for (int k = 0; k < kPtResBuffers; ++k) {
+    for (int k = 0; k <= kPtMaxSlots; ++k) {
         HIP_TRY(hipEventCreateWithFlags(&r->pt_fin[k], hipEventDisableTiming | hipEventReleaseToDevice));
     }
     return RT_OK;
@@ -840,17 +842,42 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     if (pipe) {
         int rc = ensure_pipe_streams(r);
         if (rc != RT_OK) return rc;
+        if (need > r->pt_need) {
+            // as many slots as fit beside 8 GB of headroom (at least 2), decided again whenever a
+            // frame needs larger slots: every pending frame is done, slots past the count freed
+            HIP_TRY(hipDeviceSynchronize());
+            size_t free_b = 0, total_b = 0;
+            HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+            double avail = (double)free_b;
+            for (size_t b : r->pt_bytes) avail += (double)b;
+            uint32_t k = s->pt_slots;
+            while (k > 2 && (double)k * need + (8ull << 30) > avail) --k;
+            for (uint32_t j = k; j < (uint32_t)kPtMaxSlots; ++j) {
+                if (r->d_pt[j]) HIP_TRY(hipFree(r->d_pt[j]));
+                r->d_pt[j] = nullptr;
+                r->pt_bytes[j] = 0;
+            }
+            for (uint32_t j = k + 1; j <= (uint32_t)kPtMaxSlots; ++j) {
+                if (r->d_res[j]) HIP_TRY(hipFree(r->d_res[j]));
+                r->d_res[j] = nullptr;
+                r->res_bytes[j] = 0;
+            }
+            r->pt_nslots = k;
+            r->pt_need = need;
+            r->pt_slot = r->pt_parity = 0;
+            for (bool &f : r->pt_fin_set) f = false;
+        }
         par = r->pt_parity;
-        r->pt_parity = (par + 1) % kPtResBuffers;
+        r->pt_parity = (par + 1) % (int)(r->pt_nslots + 1);
         if ((rc = ensure_res(r, par, res_need)) != RT_OK) return rc;
     }
-    bool used[2] = {false, false};
+    bool used[kPtMaxSlots] = {};
     const size_t lds = stack_bytes(s);
     // levels are compacted level by level until one is small enough to drain (k_pt_level)
     const uint32_t drain_level = s->pt_drain_level;
     for (uint32_t s0 = 0; s0 < F.spp; s0 += (uint32_t)batch) {
         const int k = pipe ? r->pt_slot : 0;
-        if (pipe) r->pt_slot ^= 1;
+        if (pipe) r->pt_slot = (r->pt_slot + 1) % (int)r->pt_nslots;
         hipStream_t X = pipe ? r->pt_stream[k] : st;
         const size_t slot_need = need + (pipe ? 0 : (size_t)np * 16u + 256u);   // serial: + the results
         if (slot_need > r->pt_bytes[k]) {
@@ -915,7 +942,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     if (pipe) {
         // one finishing pass on the caller's stream: every sample of the frame in sample order
         // (the same float sums as the batched running sum), after every batch's levels
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < (int)r->pt_nslots; ++k)
             if (used[k]) {
                 HIP_TRY(hipEventRecord(r->pt_lv[k], r->pt_stream[k]));
                 HIP_TRY(hipStreamWaitEvent(st, r->pt_lv[k], 0));
@@ -1697,13 +1724,13 @@ int rt_renderer_destroy(rt_renderer *r) {
     (void)hipFree(r->d_acc);
     (void)hipFree(r->d_counters);
     if (r->d_rgb) (void)hipFree(r->d_rgb);
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < kPtMaxSlots; ++k)
         if (r->d_pt[k]) (void)hipFree(r->d_pt[k]);
     for (int k = 0; k < kPsMaxDepth; ++k) {
         if (r->pt_stream[k]) (void)hipStreamDestroy(r->pt_stream[k]);
         if (r->pt_lv[k]) (void)hipEventDestroy(r->pt_lv[k]);
     }
-    for (int k = 0; k < kPtResBuffers; ++k) {
+    for (int k = 0; k <= kPtMaxSlots; ++k) {
         if (r->d_res[k]) (void)hipFree(r->d_res[k]);
         if (r->pt_fin[k]) (void)hipEventDestroy(r->pt_fin[k]);
     }
@@ -1875,7 +1902,7 @@ int rt_renderer_device_bytes(const rt_renderer *r, uint64_t *bytes, uint32_t *ps
     const uint64_t tiles = (uint64_t)((r->W + 7) / 8) * ((r->H + 7) / 8);
     uint64_t b = 16u * pix + kCounterSlots * 8u * sizeof(unsigned long long);   // accumulator, counters
     if (r->d_rgb) b += 4u * pix;
-    for (int k = 0; k < 2; ++k) b += r->pt_bytes[k];
+    for (size_t k : r->pt_bytes) b += k;
     for (size_t k : r->res_bytes) b += k;
     if (r->d_sum) b += tiles * 64u * sizeof(float4);
     b += r->samples_bytes;

@@ -499,20 +499,24 @@ def test_wavefront_equals_one_kernel_path_tracer(rt, torch, monkeypatch, recipe,
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("recipe,W,H,mem", [("cfg3", 200, 120, "3"), ("cfg5", 96, 64, "12288")])
-def test_pipelined_batches_equal_serial(rt, torch, monkeypatch, recipe, W, H, mem):
-    """Sample batches alternating two path-state slots and streams (the default) against the
+@pytest.mark.parametrize("recipe,W,H,mem,slots", [("cfg3", 200, 120, "3", "4"), ("cfg5", 96, 64, "12288", "4"),
+                                                  ("cfg3", 200, 120, "3", "2"), ("cfg5", 96, 64, "12288", "3")])
+def test_pipelined_batches_equal_serial(rt, torch, monkeypatch, recipe, W, H, mem, slots):
+    """Sample batches rotating over `slots` path-state slots and streams (default 4) against the
     one-slot path on the caller's stream: frames submitted back to back with no host sync in
-    between (the next frame's bounce levels overlap this frame's tail), several batches per
-    frame (3 MB of path state) or one, primary+shadow frames and a reset interleaved -- every
-    frame, the accumulator and the ray counters bit for bit."""
+    between (the next frames' bounce levels overlap this frame's tail), several batches per
+    frame (3 MB of path state) or one, frames needing larger slots (the slot count is decided
+    again), primary+shadow frames and a reset interleaved -- every frame, the accumulator and
+    the ray counters bit for bit."""
     monkeypatch.setenv("RT_PT_MEM_MB", mem)
+    monkeypatch.setenv("RT_PT_SLOTS", slots)
     monkeypatch.setenv("RT_PT_PIPELINE", "0")
     s0 = rt.Scene.recipe(recipe)
     monkeypatch.setenv("RT_PT_PIPELINE", "1")
     s1 = rt.Scene.recipe(recipe)
     r0, r1 = rt.Renderer(s0, W, H), rt.Renderer(s1, W, H)
-    plan = [(4, 4, False), (4, 4, False), (1, 1, False), (8, 6, False), (2, 10, True), (4, 4, False)]
+    plan = [(4, 4, False), (4, 4, False), (1, 1, False), (8, 6, False), (2, 10, True), (4, 4, False),
+            (4, 4, False), (2, 6, False), (4, 4, False), (4, 4, False), (3, 5, False)]
     st = torch.cuda.Stream()
     outs = []
     with torch.cuda.stream(st):

@@ -36,9 +36,9 @@ for s in "$@"; do
             step bench_cfg4 300 python bench.py --config 4 --steps 30 --warmup 5 --no-cpu-baseline
             step bench_cfg5 300 python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline ;;
         profcfg)   # kernel trace + PMC passes of every config's bench run, summarised by tools/roofline.py
-            # serial frames (RT_PS_PIPELINE=0): overlapped kernels share the CUs, so their trace
-            # durations would not be one kernel's; no 720p companion run (same kernel name)
-            export RT_PS_PIPELINE=0
+            # serial frames (RT_PS_PIPELINE=0, RT_PT_PIPELINE=0): overlapped kernels share the CUs,
+            # so their trace durations would not be one kernel's; no 720p companion run (same kernel name)
+            export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0
             for c in ${PROF_CONFIGS:-2 3 4 5}; do
                 if [ $c = 2 ] || [ $c = 4 ]; then n=60; k="k_render<0, 1, false>"; else n=6; k="k_pt_lanes"; fi
                 b="python bench.py --config $c --steps $n --warmup 2 --no-cpu-baseline --no-companion --ramp-seconds 0.3"
@@ -49,7 +49,7 @@ for s in "$@"; do
                 step pmc_c${c}_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pc$c/tcc -o pmc --output-format csv -- $b
                 step sum_c$c 60 python tools/roofline.py summarize cfg$c "$k" gpurun_out/pc$c/trace gpurun_out/pc$c/fetch gpurun_out/pc$c/write gpurun_out/pc$c/sq gpurun_out/pc$c/tcc --tail 0.5 --out gpurun_out/pmc_summary.json
             done
-            unset RT_PS_PIPELINE ;;
+            unset RT_PS_PIPELINE RT_PT_PIPELINE ;;
         prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 100 --warmup 5 --no-cpu-baseline ;;
         listpmc) step listpmc 120 rocprofv3 -L ;;
         pmclds)

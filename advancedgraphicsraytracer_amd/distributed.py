@@ -136,6 +136,12 @@ class ShardedFrame:
         pass
 
 
+class NativeCommUnavailable(RuntimeError):
+    """The C++ RCCL communicator could not be set up; raised on every rank of the group
+    together, so the caller can fall back to ShardedFrame (the same gather through
+    torch.distributed) without any rank being left inside a collective."""
+
+
 class NativeShardedFrame:
     """Multi-GPU frames through the C-ABI: rt_render_frame_multi renders this rank's tiles and
     runs the frame's RCCL gather from C++ (rt_multi.cpp); rank 0 assembles.  Same interface
@@ -148,14 +154,29 @@ class NativeShardedFrame:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.device = torch.device("cuda", renderer.scene.device) if device is None else torch.device(device)
+        # Set-up fails on every rank together (NativeCommUnavailable), never on one rank while
+        # its peers wait in a collective: rank 0's unique-id failure is broadcast as None, and
+        # every rank's rt_comm_create result is min-reduced before anyone goes on.
         uid = (C.c_uint8 * RT_COMM_ID_BYTES)()
+        box = [None]
         if self.rank == 0:
-            _check(self.L.rt_comm_unique_id(uid))
-        box = [bytes(uid)]
+            rc = self.L.rt_comm_unique_id(uid)
+            box = [bytes(uid) if rc == 0 else None]
+            err = "" if rc == 0 else self.L.rt_last_error().decode(errors="replace")
         dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        if box[0] is None:
+            raise NativeCommUnavailable("rt_comm_unique_id failed on rank 0" + (f": {err}" if self.rank == 0 else ""))
         uid = (C.c_uint8 * RT_COMM_ID_BYTES).from_buffer_copy(box[0])
         self.h = C.c_void_p()
-        _check(self.L.rt_comm_create(uid, self.rank, self.world, self.device.index or 0, C.byref(self.h)))
+        rc = self.L.rt_comm_create(uid, self.rank, self.world, self.device.index or 0, C.byref(self.h))
+        err = "" if rc == 0 else self.L.rt_last_error().decode(errors="replace")
+        ok = torch.tensor([1 if rc == 0 else 0], device=self.device if dist.get_backend(group) == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if not int(ok.item()):
+            if rc == 0:
+                self.L.rt_comm_destroy(self.h)
+            self.h = None
+            raise NativeCommUnavailable(f"rt_comm_create failed on some rank (this rank: {err or 'ok'})")
         self.frame = torch.zeros(renderer.width * renderer.height, dtype=torch.int32, device=self.device)
         self._pipelined, self._timing_flag = MULTI_PIPELINED, (MULTI_TIMING if timing else 0)
         # RT_MULTI_BALANCED: the cost-balanced compact tile deal from a parameter set's 7th frame on

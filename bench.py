@@ -237,15 +237,22 @@ def main():
     sptr = stream.cuda_stream
     frame_out = torch.zeros(W * H, dtype=torch.int32, device=f"cuda:{device}")
     sharded = None
+    native_fallback = None
     if world > 1:
-        from advancedgraphicsraytracer_amd.distributed import NativeShardedFrame, ShardedFrame
+        from advancedgraphicsraytracer_amd.distributed import NativeCommUnavailable, NativeShardedFrame, ShardedFrame
         if backend == "nccl":   # the product path: RCCL gather from C++ (rt_render_frame_multi)
             # strong scaling renders compact cost-balanced screen regions per rank from a parameter
             # set's 7th frame on (RT_MULTI_BALANCED: each GPU's caches hold its region's part of
             # the scene); weak scaling keeps the interleaved deal, whose 1/N shards at spp N are
             # statistically identical (tools/shard_time.py)
-            sharded = NativeShardedFrame(rend, device=torch.device("cuda", device), balanced=args.scaling == "strong")
-        else:
+            try:
+                sharded = NativeShardedFrame(rend, device=torch.device("cuda", device), balanced=args.scaling == "strong")
+            except NativeCommUnavailable as e:   # raised on every rank together: same gather via torch's RCCL
+                if rank == 0:
+                    print(f"bench: native RCCL communicator unavailable ({e}); torch.distributed gather instead",
+                          file=sys.stderr, flush=True)
+                native_fallback = str(e)
+        if sharded is None:
             sharded = ShardedFrame(rend, device=torch.device("cuda", device))
 
     def step(i, events=None):
@@ -341,6 +348,8 @@ def main():
                      "gather_ms_per_frame_max_rank": round(per[1].item(), 4)}
         else:
             multi = {"exchange": f"torch.distributed gather ({backend})"}
+            if native_fallback:
+                multi["native_comm_unavailable"] = native_fallback
     if dist:
         dist.all_reduce(local_rays, op=dist.ReduceOp.SUM)
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)

@@ -200,9 +200,17 @@ constexpr int kTuneGroup = 4;
 constexpr int kWalkTimed = 4 * kTuneGroup;
 constexpr int kTuneDecide = 1 + kWalkTimed, kTuneDone = kTuneDecide + 1;
 
-uint32_t pick_stack(uint32_t depth) {   // entries needed <= tree depth; round up to 8
+// LDS stack entries per lane: a traversal pushes at most one entry per tree level, so the tree
+// depth is enough.  Rounding it up to 8 cost occupancy where the stacks bound the workgroups
+// per CU (mig29 x16: 26 levels, 32 KB per workgroup -> 5 per CU; exact: 26 KB -> 6): CFG3-sub
+// 1.79 -> 1.65 ms, CFG5-sub 7.58 -> 7.47 ms, mig29 x16 0.330 -> 0.321 ms, TEAPOT-F unchanged
+// (round 3, profiles/r03/ab_stack/).
+#ifndef RT_STACK_ROUND
+#define RT_STACK_ROUND 1u
+#endif
+uint32_t pick_stack(uint32_t depth) {   // entries needed <= tree depth (rounded up to RT_STACK_ROUND)
     uint32_t need = depth < 2 ? 2 : depth;
-    return (need + 7u) & ~7u;
+    return (need + RT_STACK_ROUND - 1u) / RT_STACK_ROUND * RT_STACK_ROUND;
 }
 
 int material_flag(const rt_material &m, float diffuse, float specular) {   // getFlag overrides

@@ -25,8 +25,9 @@ import sys
 import time
 
 
-def _path_traced(argv):
-    """Trace depth > 1 for this command line (--config / --depth), before anything loads HIP."""
+def _wants_8_queues(argv):
+    """Path tracing (trace depth > 1) or config 4, for this command line (--config / --depth),
+    before anything loads HIP."""
     cfg, depth = 2, None
     for i, a in enumerate(argv):
         key, _, val = a.partition("=")
@@ -36,7 +37,7 @@ def _path_traced(argv):
             cfg = int(val)
         elif key == "--depth":
             depth = int(val)
-    return (depth if depth is not None else {3: 4, 5: 10}.get(cfg, 1)) > 1
+    return (depth if depth is not None else {3: 4, 5: 10}.get(cfg, 1)) > 1 or cfg == 4
 
 
 # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process (4 by default).  Path
@@ -45,8 +46,10 @@ def _path_traced(argv):
 # ms (profiles/r02/bench_pipe_bhq*.json).  Multi-GPU frames (N > 1) too, since overlapped
 # primary+shadow frames: their two renderer streams and the communicator's stream then no longer
 # share a queue with the caller's (world-1 multi frame, mig29 x16: 0.471 -> 0.327 ms; TEAPOT-F
-# 0.128 either way; profiles/r02/multi_overhead_hwq8.log).  Single-GPU primary+shadow runs keep
-# HIP's default.  Set before HIP initialises.
+# 0.128 either way; profiles/r02/multi_overhead_hwq8.log).  Config 4 at N = 1 too: its frames in
+# flight (up to 6 renderer streams) no longer share queues -- 0.3045 / 0.3005 -> 0.280 / 0.270 ms
+# (profiles/r03/hwq_ab/).  Config 2 keeps HIP's default: with 8 queues its timed choice drifted to
+# 2 frames in flight and the frame to 0.108-0.120 ms.  Set before HIP initialises.
 # The box may export its own value (HIP's default is 4): the bench sets 8 explicitly where its
 # design needs it and records the value in effect (config.hip_hw_queues).  --hw-queues N
 # overrides; never above 32 (the pool refuses more).
@@ -55,7 +58,7 @@ _HWQ_ARG = next((a.partition("=")[2] or (sys.argv[i + 2] if i + 2 < len(sys.argv
                  for i, a in enumerate(sys.argv[1:]) if a.startswith("--hw-queues")), None)
 if _HWQ_ARG:
     os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, int(_HWQ_ARG))))
-elif _path_traced(sys.argv[1:]) or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+elif _wants_8_queues(sys.argv[1:]) or int(os.environ.get("WORLD_SIZE", "1")) > 1:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import numpy as np  # noqa: E402

@@ -64,7 +64,7 @@ struct rt_scene {
     uint32_t pt_drain_level = 64;   // bounce level from which the wavefront always drains (64 = never forced)
     double pt_drain_rounds = 1.0;   // ... and it drains any level holding <= this many rounds of resident lanes
     bool tile_order = true;         // measured-cost (longest first) tile order (RT_TILE_ORDER=0: off)
-    uint32_t split_units = 20000;   // sample split below ~5 rounds of the 4096 resident waves
+    uint32_t split_units = 40000;   // sample split below this many tiles (1080p = 32,400 tiles)
     bool xcd_order = false;         // measured order grouped by XCD: blocks b, b + 8, ... (one XCD) render
                                     // one compact screen region of 1/8 of the frame's cost (L2 locality)
     int32_t heavy_split = -1;       // primary+shadow frames: the costliest tiles run as two half-tile
@@ -1219,8 +1219,11 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     // round of whole-tile waves, as long as its slowest tile)
     F.nchunks = 1;
     const bool wavefront = mode == RT_MODE_PATH && depth >= 2 && s->pt_wavefront;
-    // (measured on TEAPOT-F shards, tools/shard_time.py: no split while the tiles alone make
-    // ~5 rounds; below that, split until ~10 rounds, chunks of equal sample counts)
+    // (first measured on TEAPOT-F shards, tools/shard_time.py: split below ~5 rounds of
+    // waves, until ~10 rounds, chunks of equal sample counts.  Round 3: whole 1080p frames at
+    // spp > 1 gain from it too -- CFG5-sub scene spp 16 2.41 -> 1.44 ms, mig29 x16 spp 4 1.49
+    // -> 0.76 ms, TEAPOT-F spp 4 0.390 -> 0.386 ms, frames identical (profiles/r03/split_ab/) --
+    // so the threshold is 40,000 tiles instead of 20,000; 80,000 measured the same or slower)
     if (p->spp > 1 && mode != RT_MODE_PACKET && !wavefront && F.ntiles_local < s->split_units)
         while (F.ntiles_local * F.nchunks < 2u * s->split_units && F.nchunks < p->spp) {
             uint32_t d = F.nchunks + 1;                  // next divisor of spp: equal chunks

@@ -360,8 +360,13 @@ def main():
     wall = t_max.item()
     overlap = rend.overlap()
     in_flight = rend.overlap_depth()
+    choices = rend.choices() if args.depth == 1 else None   # the renderer's timed camera-walk / split choices
     companion = None
     if world == 1 and args.depth == 1 and (W, H) == (1920, 1080) and not args.no_companion:   # the metric's other frame size
+        # the measured renderer is done: free its streams first, so that the companion's
+        # frames-in-flight streams get hardware queues of their own (with 8 queues a second
+        # renderer beside the first ran config 4's 720p frames at 0.234 instead of 0.168 ms)
+        rend.close()
         companion = companion_rate(scene, 1280, 720, spp, args.depth, stream, device)
 
     if rank == 0:
@@ -417,6 +422,8 @@ def main():
             line["overlapped_frames"] = {"state": overlap[0], "in_flight": in_flight[0], "timed_groups_ms": groups,
                                          "groups": ("frames in flight serial, 2, 4, 6, 6, 4, 2, serial" if len(groups) == 8
                                                     else "frames in flight serial, 2, 2, serial") + " (8 frames each)"}
+            if choices is not None:   # walk 0 lane / 1 wave, split 0 plain / 1 half tiles; groups A, B, B, A
+                line["timed_choices"] = choices
         if multi:
             line["multi_gpu"] = multi
         if companion:

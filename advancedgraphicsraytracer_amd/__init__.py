@@ -21,7 +21,7 @@ LIB_PATH = os.path.abspath(os.environ.get("RTAMD_LIB", os.path.join(PKG_DIR, "li
 DATA_DIR = os.path.join(PKG_DIR, "data")
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "rt_amd.h")
 
-ABI_VERSION = 3   # include/rt_amd.h RT_ABI_VERSION
+ABI_VERSION = 4   # include/rt_amd.h RT_ABI_VERSION
 RT_OK, RT_ERR_INVALID, RT_ERR_NO_DEVICE, RT_ERR_HIP, RT_ERR_IO, RT_ERR_UNSUPPORTED, RT_ERR_COMM = 0, -1, -2, -3, -4, -5, -6
 RT_COMM_ID_BYTES = 128
 MULTI_PIPELINED, MULTI_TIMING, MULTI_BALANCED = 1, 2, 4
@@ -31,6 +31,7 @@ MODE_PATH = 0
 MODE_WHITTED = 1
 MODE_PACKET = 2
 WALK_LANE, WALK_WAVE, WALK_AUTO = 0, 1, 2
+WALK_CHECK_OFF, WALK_CHECK_COUNT, WALK_CHECK_VERIFY = 0, 1, 2
 BVH_PLAIN, BVH_SBVH = 0, 1
 # renderer.h:9, renderer.h:13, renderer.cpp:105 (TracePacket's bounces: Trace's default depth)
 DEFAULT_DEPTH = {MODE_PATH: 10, MODE_WHITTED: 20, MODE_PACKET: 10}
@@ -149,6 +150,8 @@ def lib():
         "rt_render_frame_multi": ([vp, vp, C.POINTER(Camera), C.POINTER(FrameParams), vp, u32, vp], C.c_int),
         "rt_multi_flush": ([vp, vp, vp, vp], C.c_int),
         "rt_comm_timing": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64)], C.c_int),
+        "rt_comm_deal_info": ([vp, C.POINTER(C.c_int), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                               C.POINTER(C.c_uint64)], C.c_int),
         "rt_camera_default": ([u32, u32, C.POINTER(Camera)], C.c_int),
         "rt_renderer_create": ([vp, u32, u32, C.POINTER(vp)], C.c_int),
         "rt_renderer_destroy": ([vp], C.c_int),
@@ -167,6 +170,8 @@ def lib():
         "rt_renderer_device_bytes": ([vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)], C.c_int),
         "rt_renderer_tile_costs": ([vp, C.POINTER(u32), u32, C.POINTER(u32)], C.c_int),
         "rt_renderer_choices": ([vp, C.POINTER(C.c_int), C.POINTER(C.c_int), fp, fp], C.c_int),
+        "rt_renderer_set_walk_check": ([vp, C.c_int], C.c_int),
+        "rt_renderer_walk_stats": ([vp, C.POINTER(C.c_uint64)], C.c_int),
         "rt_renderer_stream": ([vp, C.POINTER(vp)], C.c_int),
         "rt_frame_kernel_name": ([vp, C.POINTER(FrameParams)], C.c_char_p),
         "rt_synchronize": ([vp], C.c_int),
@@ -736,6 +741,16 @@ class Renderer:
         _check(self.L.rt_renderer_choices(self.h, C.byref(w), C.byref(sp), _fptr(wm), _fptr(sm)))
         return {"walk": w.value, "split": sp.value, "walk_ms": [round(float(x), 4) for x in wm],
                 "split_ms": [round(float(x), 4) for x in sm]}
+
+    def set_walk_check(self, level):
+        """WALK_CHECK_OFF (default) / WALK_CHECK_COUNT / WALK_CHECK_VERIFY (rt_renderer_set_walk_check)."""
+        _check(self.L.rt_renderer_set_walk_check(self.h, level))
+
+    def walk_stats(self):
+        """The wave camera walk's cumulative counters: {walked, margin_boxes, retraced, verify_mismatch}."""
+        out = (C.c_uint64 * 4)()
+        _check(self.L.rt_renderer_walk_stats(self.h, out))
+        return {"walked": int(out[0]), "margin_boxes": int(out[1]), "retraced": int(out[2]), "verify_mismatch": int(out[3])}
 
     def tile_costs(self):
         """Per-local-tile wave cycles behind the measured tile order (empty until recorded)."""

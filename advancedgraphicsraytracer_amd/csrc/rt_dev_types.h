@@ -22,9 +22,6 @@ struct DevMaterial {
 
 struct SceneView {
     const float4 *__restrict__ nodes;   // 2 float4 per node
-    const float4 *__restrict__ pairs;   // 4 float4 per child pair (X, Y, Z, words), pair k at 4k
-    const float4 *__restrict__ pairs48; // 3 float4 per child pair (X, Y, Z), pair k at 3k
-    const uint32_t *__restrict__ words; // node words (leftFirst << 8 | count) by node index
     const float4 *__restrict__ prims;   // 3 float4 per leaf slot
     const float4 *__restrict__ shade;   // 2 float4 per primitive id
     const DevMaterial *__restrict__ mats;
@@ -44,11 +41,12 @@ struct SceneView {
     uint32_t root_word;
     int bounds_finite;                  // every node bound is a finite float
     uint32_t stack_entries;             // LDS stack entries per lane
-    uint32_t node_f4;                   // node array size in float4s
-    uint32_t p48_f4, words_n;           // pairs48 size in float4s, words count
     int wave_primary;                   // camera rays take the wave-coherent walk
-    uint32_t tl_nodes;                  // RT_PT_TREELET: nodes [0, tl_nodes) (BFS-numbered top pairs)
-                                        // are copied to LDS by the lane kernel; 0 = off
+    int walk_check;                     // RT_WALK_CHECK_*: what the walk counts / verifies
+    unsigned long long *walk_stats;     // the renderer's counter slots (kCounterSlots x 8 u64), set per
+                                        // launch: the wave walk adds [2] boxes entered within its
+                                        // cull margin, [3] lanes re-traced in the reference order,
+                                        // [4] camera rays it walked, [5] RT_WALK_VERIFY mismatches
 };
 
 // Ray counters are spread over kCounterSlots 64-byte slots (wave w adds into slot
@@ -72,15 +70,15 @@ struct FrameArgs {
     float4 *acc;
     uint32_t *out;
     unsigned long long *counters;       // kCounterSlots slots of 8 u64 (64 B): [0] shadow rays, [1] bounce rays
+                                        // ([2..5] the camera walk's counters, SceneView::walk_stats)
 };
 
 // One launch of the frame kernel family (Renderer::Tick): integrator mode, Trace depth
-// bucket, textured sky, LDS-node kernel.
+// bucket, textured sky.
 struct FrameLaunch {
     int mode;        // RT_MODE_*
     int md;          // depth bucket: 1, 4, 10 or 32
     bool tex;        // non-constant sky texture
-    int lds;         // 0 global nodes; 64: k_render_lds (1024 threads); 48: k_render_lds48 (512)
     dim3 grid, block;
     size_t lds_bytes;
     hipStream_t stream;
@@ -117,6 +115,8 @@ struct PathArgs {
     uint32_t *queue_in, *queue_out;
     uint32_t *qcount;
     float4 *sum;
+    uint32_t *tile_cost;                 // level 0: if set, each local tile's wave cycles (summed over its
+                                         // samples) are added here -- a multi-GPU deal's cost map
 };
 
 // Batched Renderer::Trace / WhittedTrace on caller rays (rt_trace): one lane per ray.
@@ -153,12 +153,6 @@ struct TraceArgs {
 RT_DECLARE_LAUNCHERS(kcore)
 RT_DECLARE_LAUNCHERS(kext)
 #undef RT_DECLARE_LAUNCHERS
-// RT_PT_SORT: reorder a bounce level's queue (P.queue_in, P.level) by direction octant + origin
-// cell into `sorted` (same segment layout; the level's queue counts are rewritten); work =
-// pt_sort_work_bytes(), keys = 2 B per path of the batch
-void launch_pt_sort(const SceneView &S, const PathArgs &P, uint32_t *sorted, uint32_t *work, uint16_t *keys,
-                    uint32_t num_cus, hipStream_t st);
-size_t pt_sort_work_bytes();
 // where: per global tile (shard << 24 | local tile) of an explicit deal; nullptr = interleaved
 void launch_assemble(const uint32_t *gathered, uint32_t cap, uint32_t nshards, const uint32_t *where, uint32_t tiles_x,
                      uint32_t ntiles, uint32_t W, uint32_t H, uint32_t *out, hipStream_t st);

@@ -53,7 +53,6 @@ struct rt_scene {
     Bvh bvh;
     uint32_t num_prims = 0;
     uint32_t stack_depth = 0;   // LDS stack entries per lane
-    int lds_kernel = 0;         // primary+shadow frames: 64 = k_render_lds, 48 = k_render_lds48, 0 = global nodes
     uint32_t num_cus = 256;     // persistent grid size of k_render_lds
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
     int walk = RT_WALK_LANE;    // camera-ray walk of the global-node primary+shadow kernel
@@ -69,7 +68,6 @@ struct rt_scene {
                                     // one compact screen region of 1/8 of the frame's cost (L2 locality)
     int32_t heavy_split = -1;       // primary+shadow frames: the costliest tiles run as two half-tile
                                     // waves (RT_SPLIT_HEAVY = count; -1: ntiles / 32)
-    uint32_t pt_sort_levels = 0;    // bounce levels 1..n reordered by direction octant + origin cell (RT_PT_SORT)
     uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per slot (two when pipelined): 12 GB
                                               // of the 288 GB HBM holds all 16 spp of a 1080p depth-10 frame
     bool pt_pipeline = true;        // sample batches alternate path-state slots and streams
@@ -84,7 +82,7 @@ struct rt_scene {
                                     // (RT_TUNE_DELAY_MS): the clocks ramp over ~0.1 s, and choices
                                     // timed on the first frames at low clocks came out wrong
     void *d_nodes = nullptr, *d_prims = nullptr, *d_shade = nullptr, *d_mats = nullptr, *d_sky = nullptr;
-    void *d_xprims = nullptr, *d_tex = nullptr, *d_pairs = nullptr, *d_pairs48 = nullptr, *d_words = nullptr;
+    void *d_xprims = nullptr, *d_tex = nullptr;
     void *d_scratch = nullptr;  // staging for the host-pointer batched calls
     size_t scratch_bytes = 0;
     hipStream_t stream = nullptr;
@@ -111,7 +109,8 @@ struct rt_renderer {
     std::vector<uint32_t> host_cost;   // the cost map the active order was sorted from (local tiles)
     uint32_t order_n = 0;
     uint64_t order_key = 0;
-    int order_state = 0;        // 0 idle, 1 costs recorded, 2 order active
+    int order_state = 0;        // 0 idle, 1 costs recorded, 2 order active, 3 costs held without an
+                                // order (path-traced frames)
     uint32_t order_split = 0;   // leading tiles of the split order that run as two half-tile units
     int split_phase = -1;       // -1 decided / not tried; 0 .. 4 kTuneGroup - 1 timing frames in groups
                                 // (plain, split, split, plain), 4 kTuneGroup decide
@@ -120,6 +119,8 @@ struct rt_renderer {
     float split_ms[4] = {};
     int tune = 0;                   // camera walk: 0 warm-up, 1 .. kWalkTimed timed frames, kTuneDecide, kTuneDone
     bool wave = false;
+    uint64_t tune_key = 0;          // the parameter set whose frames the walk timing ran on
+    int walk_check = RT_WALK_CHECK_OFF;     // rt_renderer_set_walk_check
     hipEvent_t tev[8] = {};         // walk timing: events 2g, 2g + 1 around group g
     // wavefront path tracer (PathArgs): two path-state slots (state, records, queues), grown on
     // demand, each owned by one of the renderer's two path streams.  Sample batches alternate
@@ -157,6 +158,7 @@ struct rt_renderer {
     uint32_t ps_prev = 0;           // frames in flight of the previous eligible frame (0 serial)
     hipEvent_t pev[16] = {};
     hipEvent_t ps_join = nullptr;   // caller's stream -> overlap stream, on a switch to overlapped
+    hipEvent_t cost_ev = nullptr;   // path-traced frames: the cost map was cleared (caller's stream)
     float ps_ms[8] = {};
     // the overlapped frames' per-sample results, frame n in buffer n % buffers (kernel on
     // renderer stream n % depth): frame n + buffers waits for the finishing pass of frame n only,
@@ -238,43 +240,6 @@ int material_flag(const rt_material &m, float diffuse, float specular) {   // ge
 
 constexpr uint32_t kMaxNodes = 1u << 24;   // the packed word's leftFirst field is 24 bits wide
 
-// The first `want` sibling pairs in breadth-first order from the root (pair 0 = root + the
-// unused node 1 stays first), the remaining pairs in their original relative (DFS) order;
-// interior leftFirst values renumbered.  Returns the number of leading pairs placed
-// breadth-first (<= want): the lane kernel's LDS treelet.
-uint32_t bfs_top_order(const Bvh &b, uint32_t want, std::vector<Node> &out) {
-    const uint32_t npairs = (b.nodes_used + 1) / 2;
-    std::vector<uint32_t> newof(npairs, UINT32_MAX), order;
-    order.reserve(npairs);
-    newof[0] = 0;
-    order.push_back(0);
-    std::vector<uint32_t> queue;
-    auto kids = [&](uint32_t node) {
-        const Node &nd = b.nodes[node];
-        if (nd.count == 0 && nd.leftFirst >= 2) queue.push_back(nd.leftFirst / 2);
-    };
-    kids(0);
-    for (size_t qi = 0; qi < queue.size() && order.size() < want; ++qi) {
-        const uint32_t p = queue[qi];
-        if (newof[p] != UINT32_MAX) continue;
-        newof[p] = (uint32_t)order.size();
-        order.push_back(p);
-        kids(2 * p);
-        kids(2 * p + 1);
-    }
-    const uint32_t placed = (uint32_t)order.size();
-    for (uint32_t p = 0; p < npairs; ++p)
-        if (newof[p] == UINT32_MAX) { newof[p] = (uint32_t)order.size(); order.push_back(p); }
-    out.assign(b.nodes.begin(), b.nodes.begin() + b.nodes_used);
-    for (uint32_t p = 0; p < npairs; ++p)
-        for (uint32_t c = 0; c < 2 && 2 * p + c < b.nodes_used; ++c) {
-            Node nd = b.nodes[2 * p + c];
-            if (nd.count == 0 && !(p == 0 && c == 1)) nd.leftFirst = 2 * newof[nd.leftFirst / 2];
-            out[2 * newof[p] + c] = nd;
-        }
-    return placed;
-}
-
 int validate_bvh(const Bvh &b, uint32_t n) {
     if (b.nodes_used < 2 || b.nodes_used > b.nodes.size()) return fail(RT_ERR_INVALID, "BVH node count out of range");
     std::vector<uint8_t> seen(n, 0);
@@ -306,8 +271,7 @@ void free_scene(rt_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     (void)hipDeviceSynchronize();
-    void *ptrs[] = {s->d_nodes, s->d_pairs, s->d_pairs48, s->d_words, s->d_prims, s->d_shade, s->d_mats, s->d_sky, s->d_xprims, s->d_tex,
-                    s->d_scratch};
+    void *ptrs[] = {s->d_nodes, s->d_prims, s->d_shade, s->d_mats, s->d_sky, s->d_xprims, s->d_tex, s->d_scratch};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -334,8 +298,6 @@ inline f3 tvec_host(float4 r0, float4 r1, float4 r2, f3 a) {
     const float M[12] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w};
     return tvec(M, a);
 }
-
-size_t lds48_scene_bytes(const rt_scene *s);
 
 int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (!d || !out || !d->prims || d->num_prims == 0 || !d->materials || d->num_materials == 0)
@@ -424,45 +386,14 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (s->bvh.depth > 64) { delete s; return fail(RT_ERR_UNSUPPORTED, "BVH deeper than 64 (the reference's stack[64])"); }
     s->stack_depth = pick_stack(s->bvh.depth);
 
-    // ---- device node order: the reference's (DFS) order, or with RT_PT_TREELET the top pairs
-    // renumbered breadth-first so that the lane kernel's LDS copy of nodes [0, 2 T) holds the
-    // top of the tree (traversal order and arithmetic do not depend on where a node is stored)
-    uint32_t tl_pairs = 0;
-    if (const char *e = std::getenv("RT_PT_TREELET")) {
-        // LDS left beside the 1024-lane stacks (160 KB per CU, one workgroup)
-        const long budget = 160l * 1024 - (long)s->stack_depth * 1024 * 4 - 1024;
-        const long want = std::atol(e) > 1 ? std::atol(e) : budget / 64;
-        if (std::atoi(e) != 0 && budget >= 64 * 64) tl_pairs = (uint32_t)std::min<long>(want, budget / 64);
-    }
-    std::vector<Node> bfs_nodes;
-    if (tl_pairs) tl_pairs = bfs_top_order(s->bvh, tl_pairs, bfs_nodes);
-    const std::vector<Node> &dn = tl_pairs ? bfs_nodes : s->bvh.nodes;
-
     // ---- device node array: packed (leftFirst << 8 | count) word in b.z
     std::vector<float4> nodes(2 * (size_t)s->bvh.nodes_used);
     for (uint32_t i = 0; i < s->bvh.nodes_used; ++i) {
-        const Node &nd = dn[i];
+        const Node &nd = s->bvh.nodes[i];
         uint32_t word = (nd.leftFirst << 8) | nd.count;
         nodes[2 * i] = make_float4(nd.mn[0], nd.mn[1], nd.mn[2], nd.mx[0]);
         nodes[2 * i + 1] = make_float4(nd.mx[1], nd.mx[2], ubits(word), 0.0f);
     }
-    // ---- the same nodes as interleaved child pairs for the LDS kernel: pair k = nodes
-    // (2k, 2k+1) at float4 4k: X = (mn.x, mn.x', mx.x, mx.x'), Y, Z alike, then the words
-    std::vector<float4> pairs(nodes.size(), make_float4(0, 0, 0, 0));
-    for (uint32_t k = 1; 2 * k + 1 < s->bvh.nodes_used; ++k) {
-        const Node &a = dn[2 * k], &b = dn[2 * k + 1];
-        const uint32_t wa = (a.leftFirst << 8) | a.count, wb = (b.leftFirst << 8) | b.count;
-        pairs[4 * k + 0] = make_float4(a.mn[0], b.mn[0], a.mx[0], b.mx[0]);
-        pairs[4 * k + 1] = make_float4(a.mn[1], b.mn[1], a.mx[1], b.mx[1]);
-        pairs[4 * k + 2] = make_float4(a.mn[2], b.mn[2], a.mx[2], b.mx[2]);
-        pairs[4 * k + 3] = make_float4(ubits(wa), ubits(wb), 0.0f, 0.0f);
-    }
-    // ... and as 48-B pairs (X, Y, Z) plus one word per node for k_render_lds48
-    std::vector<float4> pairs48(3 * (size_t)(s->bvh.nodes_used / 2 + 1), make_float4(0, 0, 0, 0));
-    std::vector<uint32_t> words(s->bvh.nodes_used, 0u);
-    for (uint32_t k = 1; 2 * k + 1 < s->bvh.nodes_used; ++k)
-        for (int c = 0; c < 3; ++c) pairs48[3 * k + c] = pairs[4 * k + c];
-    for (uint32_t i = 0; i < s->bvh.nodes_used; ++i) words[i] = (dn[i].leftFirst << 8) | dn[i].count;
     // ---- leaf-order primitive records and per-id shading records; cubes and quads keep
     // their matrices and data in a side table (8 float4 each)
     static const float I16[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
@@ -586,9 +517,6 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 
     rc = RT_OK;
     if (rc == RT_OK) rc = upload(&s->d_nodes, nodes);
-    if (rc == RT_OK) rc = upload(&s->d_pairs, pairs);
-    if (rc == RT_OK) rc = upload(&s->d_pairs48, pairs48);
-    if (rc == RT_OK) rc = upload(&s->d_words, words);
     if (rc == RT_OK) rc = upload(&s->d_prims, prims);
     if (rc == RT_OK) rc = upload(&s->d_shade, shade);
     if (rc == RT_OK) rc = upload(&s->d_mats, mats);
@@ -601,11 +529,6 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 
     SceneView &v = s->view;
     v.nodes = (const float4 *)s->d_nodes;
-    v.pairs = (const float4 *)s->d_pairs;
-    v.pairs48 = (const float4 *)s->d_pairs48;
-    v.words = (const uint32_t *)s->d_words;
-    v.p48_f4 = (uint32_t)pairs48.size();
-    v.words_n = (uint32_t)words.size();
     v.prims = (const float4 *)s->d_prims;
     v.shade = (const float4 *)s->d_shade;
     v.mats = (const DevMaterial *)s->d_mats;
@@ -639,35 +562,23 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         v.light_invr = 1.0f / L.v[3];
         v.light_area = 4.0f * kPI * v.light_r2;                        // Primitive.h:452
     }
-    const Node &root = dn[0];
+    const Node &root = s->bvh.nodes[0];
     v.root_word = (root.leftFirst << 8) | root.count;
-    v.tl_nodes = 2u * tl_pairs;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, s->device) == hipSuccess && prop.multiProcessorCount > 0)
             s->num_cus = (uint32_t)prop.multiProcessorCount;
     }
     v.stack_entries = s->stack_depth;
-    v.node_f4 = 2u * s->bvh.nodes_used;
     // Primary+shadow frames read the nodes from global memory (L1/L2-resident, 256-thread
-    // workgroups, 5 waves/SIMD).  The LDS-node kernels -- two 512-thread workgroups per CU
-    // holding the 48-B pairs, words and u16 stacks (k_render_lds48), or one 1024-thread
-    // group with the 64-B pairs (k_render_lds) -- are opt-in (RT_LDS_KERNEL=48/64): they
-    // won while every wave's ray counter went to one atomic address, and lose by 12 % since
-    // (TEAPOT-F 0.169 vs 0.192 ms, profiles/r01/ab_kernel_choice_*.json; LDS occupancy caps
-    // them at 4 waves/SIMD).
-    s->lds_kernel = 0;
-    if (const char *e = std::getenv("RT_LDS_KERNEL")) {
-        const int k = std::atoi(e);
-        if (k == 0 || (k == 64 && (size_t)s->stack_depth * 4096u + (size_t)s->bvh.nodes_used * 32u <= 160u * 1024u) ||
-            (k == 48 && lds48_scene_bytes(s) <= 160u * 1024u))
-            s->lds_kernel = k;
-    }
+    // workgroups).  The LDS-node kernels of rounds 1-3 (48-B pairs + u16 stacks in two 512-thread
+    // workgroups per CU, or 64-B pairs in one 1024-thread group) lost by 12 % once the ray
+    // counters were spread over slots (TEAPOT-F 0.169 vs 0.192 ms, profiles/r01/ab_kernel_choice_*;
+    // LDS occupancy caps them at 4 waves/SIMD) and were removed in round 4.
     // RT_PT_WAVEFRONT=0 selects the one-kernel path tracer (k_render<path, MAXD>) for A/B runs
     if (const char *e = std::getenv("RT_PT_WAVEFRONT")) s->pt_wavefront = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_DYNAMIC")) s->pt_dynamic = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_LANES")) s->pt_lanes = std::atoi(e) != 0;
-    if (const char *e = std::getenv("RT_PT_SORT")) s->pt_sort_levels = (uint32_t)std::max(0, std::atoi(e));
     // RT_PT_DRAIN_LEVEL / RT_PT_MEM_MB: wavefront drain level and path-state budget (A/B runs)
     if (const char *e = std::getenv("RT_PT_DRAIN_LEVEL")) s->pt_drain_level = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_DRAIN_ROUNDS")) s->pt_drain_rounds = std::max(0.0, std::atof(e));
@@ -704,24 +615,8 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 }
 
 size_t stack_bytes(const rt_scene *s) { return (size_t)s->stack_depth * 256u * sizeof(uint32_t); }
-// k_render_lds: [stack_entries][1024] u32 stacks, then the node array
-// k_render_lds48: [stack_entries][512] u16 stacks, 48-B pairs, node words
-size_t lds48_scene_bytes(const rt_scene *s) {
-    return (size_t)s->stack_depth * 512u * 2u + (size_t)s->view.p48_f4 * 16u + (size_t)s->view.words_n * 4u;
-}
-size_t lds_scene_bytes(const rt_scene *s) {
-    return (size_t)s->stack_depth * 1024u * sizeof(uint32_t) + (size_t)s->bvh.nodes_used * 32u;
-}
-
 // the compiled MAXD class a Trace depth runs in
 int max_depth_class(uint32_t depth) { return depth <= 1 ? 1 : depth <= 4 ? 4 : depth <= 10 ? 10 : 32; }
-// LDS nodes pay off where registers allow 1024/512-thread workgroups without spilling:
-// the primary+shadow kernel with the constant sky; the path-tracing variants keep the
-// 256-thread global-node kernel (A/B in profiles/r01).
-int lds_kind_for(const rt_scene *s, int mode, int md) {
-    return (mode == RT_MODE_PATH && md == 1 && s->view.sky_const) ? s->lds_kernel : 0;
-}
-
 // pixels covered by a frame / shard launch (primary rays per sample)
 uint64_t frame_pixels(const rt_renderer *r, const FrameArgs &F, uint32_t shard, uint32_t nshards, uint32_t tiles_x,
                       uint32_t ntiles) {
@@ -748,8 +643,10 @@ uint64_t fnv1a(const void *d, size_t n, uint64_t h = 1469598103934665603ull) {
 
 // an explicit deal's tile list on the device (FrameArgs::tile_map); a changed list waits for
 // every frame still reading the old one
-int set_tile_map(rt_renderer *r, const uint32_t *tiles, uint32_t n, uint32_t ntiles) {
-    const uint64_t h = fnv1a(tiles, sizeof(uint32_t) * n, fnv1a(&n, sizeof(n)));
+// key != 0: the caller's identity of the list (rt_multi.cpp's deals), used instead of its hash
+int set_tile_map(rt_renderer *r, const uint32_t *tiles, uint32_t n, uint32_t ntiles, uint64_t key = 0) {
+    const uint64_t h = key ? (key * 0x9e3779b97f4a7c15ull) ^ 0x5bd1e9955bd1e995ull
+                           : fnv1a(tiles, sizeof(uint32_t) * n, fnv1a(&n, sizeof(n)));
     if (r->d_map && h == r->map_hash && r->map_host.size() == n) return RT_OK;
     std::vector<uint8_t> seen(ntiles, 0);
     for (uint32_t i = 0; i < n; ++i) {
@@ -820,11 +717,14 @@ int ensure_ps_res(rt_renderer *r, uint32_t b, uint64_t bytes) {
 // Wavefront path tracing of one frame / shard (PathArgs, rt_dev_types.h): the samples are
 // processed in batches that fit RT_PT_MEM_MB (default 12288 MB) of path state; per batch
 // one k_pt_level launch per bounce level, then k_pt_finish.
-int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex, hipStream_t st) {
+int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex, hipStream_t st,
+                    uint32_t *tile_cost = nullptr) {
     rt_scene *s = r->scene;
     // camera rays of level 0 take the wave-coherent walk when the scene forces it, or when
     // the renderer's primary+shadow frames timed it faster (RT_WALK_AUTO)
     view.wave_primary = !s->has_cubes && (s->walk == RT_WALK_WAVE || (s->walk == RT_WALK_AUTO && r->tune == kTuneDone && r->wave));
+    view.walk_stats = r->d_counters;
+    view.walk_check = r->walk_check;
     const uint64_t npix = (uint64_t)F.ntiles_local * 64u;
     // pipelined: per-sample results of the whole frame in a frame-level buffer (two by frame
     // parity, up to 2 GB each); the serial path keeps them per batch with a running sum
@@ -844,10 +744,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     const uint64_t seg_cap = ((np / 64u + kQueueSegs - 1) / kQueueSegs + 1) * 64u;
     const size_t qbytes = (size_t)seg_cap * kQueueSegs * 4u;
     const size_t cbytes = (size_t)(F.depth + 1) * (2u * kQueueSegs) * 64u;   // queue counts + head counters
-    // RT_PT_SORT: a third queue (the sorted level), 2-B keys per path and the sort's counters
-    const bool sorting = s->pt_sort_levels > 0 && F.depth >= 2;
-    const size_t sort_bytes = sorting ? qbytes + (size_t)np * 2u + pt_sort_work_bytes() + 3 * 256u : 0;
-    const size_t need = (size_t)(np * (per_path - 8u) + 2 * qbytes + cbytes + 4096u) + sort_bytes;
+    const size_t need = (size_t)(np * (per_path - 8u) + 2 * qbytes + cbytes + 4096u);
     if (!r->d_sum) {   // one float4 per pixel of the whole frame (a shard uses its first npix)
         const size_t tiles = (size_t)((r->W + 7) / 8) * ((r->H + 7) / 8);
         HIP_TRY(hipMalloc(&r->d_sum, tiles * 64u * sizeof(float4)));
@@ -908,6 +805,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         }
         // this frame's results buffer was last read by the finish of two frames ago
         if (pipe && !used[k] && r->pt_fin_set[par]) HIP_TRY(hipStreamWaitEvent(X, r->pt_fin[par], 0));
+        if (pipe && !used[k] && tile_cost) HIP_TRY(hipStreamWaitEvent(X, r->cost_ev, 0));   // the cleared cost map
         used[k] = true;
         char *b = static_cast<char *>(r->d_pt[k]);
         auto take = [&](size_t bytes) { char *q = b; b += (bytes + 255u) & ~(size_t)255u; return q; };
@@ -920,12 +818,10 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         P.qhead = P.qcount + (size_t)(F.depth + 1) * kQueueSegs * 16u;
         P.dynamic = s->pt_dynamic ? 1 : 0;
         P.rec = reinterpret_cast<float4 *>(take((size_t)(F.depth - 1) * np * 32u));
-        uint32_t *qsorted = sorting ? reinterpret_cast<uint32_t *>(take(qbytes)) : nullptr;
-        uint16_t *skeys = sorting ? reinterpret_cast<uint16_t *>(take((size_t)np * 2u)) : nullptr;
-        uint32_t *swork = sorting ? reinterpret_cast<uint32_t *>(take(pt_sort_work_bytes())) : nullptr;
         // per-path radiance, indexed (sample - s0) * npix + pixel
         P.result = pipe ? r->d_res[par] + (size_t)s0 * npix : reinterpret_cast<float4 *>(take(np * 16u));
         P.sum = r->d_sum;
+        P.tile_cost = tile_cost;
         P.drain_level = drain_level;
         P.drain_below = 0;
         P.s0 = s0;
@@ -936,10 +832,6 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
             P.level = level;
             P.queue_in = (level & 1u) ? q1 : q0;
             P.queue_out = (level & 1u) ? q0 : q1;
-            if (sorting && level >= 1 && level <= s->pt_sort_levels) {   // reorder this level's queue
-                launch_pt_sort(view, P, qsorted, swork, skeys, s->num_cus, X);
-                P.queue_in = qsorted;
-            }
             int resident = 0;
             if (level > 0 && s->pt_lanes) {             // incoherent levels: the lane state machine
                 if (s->ext) kext::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, X);
@@ -1184,7 +1076,8 @@ int tune_gate(rt_renderer *r, uint64_t key, hipStream_t st, bool &open) {
 }
 
 int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
-                  uint32_t *out, int packed, void *stream, const uint32_t *tiles = nullptr, uint32_t ntiles_map = 0) {
+                  uint32_t *out, int packed, void *stream, const uint32_t *tiles = nullptr, uint32_t ntiles_map = 0,
+                  uint64_t tiles_key = 0) {
     if (!r || !cam || !p || !out) return fail(RT_ERR_INVALID, "rt_render: null argument");
     if (p->width != r->W || p->height != r->H)
         return fail(RT_ERR_INVALID, "frame size differs from the renderer's accumulator");
@@ -1206,7 +1099,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     F.shard = shard; F.nshards = nshards; F.tiles_x = tiles_x;
     F.ntiles_local = shard < ntiles ? (ntiles - shard + nshards - 1) / nshards : 0;
     if (tiles) {   // an explicit deal (rt_render_shard_tiles)
-        int rc = set_tile_map(r, tiles, ntiles_map, ntiles);
+        int rc = set_tile_map(r, tiles, ntiles_map, ntiles, tiles_key);
         if (rc != RT_OK) return rc;
         F.ntiles_local = ntiles_map;
         F.tile_map = r->d_map;
@@ -1222,7 +1115,6 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     const int md = max_depth_class(depth);
     const bool tex = !s->view.sky_const;
     const int mode = (int)p->mode;
-    const int lds_kind = lds_kind_for(s, mode, md);
     // sample split: a frame (or a shard of one) with few tiles and several samples per
     // pixel is cut into (tile, sample chunk) units, so the dispatcher still balances about
     // s->split_units waves of uneven cost (a 1/8 shard at spp 8 would otherwise be one
@@ -1252,39 +1144,69 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         }
         F.samples = static_cast<float4 *>(r->d_samples);
     }
-    dim3 grid, block;
-    size_t lds;
-    if (lds_kind == 64) {
-        grid = dim3((F.nunits + 15) / 16);
-        block = dim3(1024);
-        lds = lds_scene_bytes(s);
-    } else if (lds_kind == 48) {
-        grid = dim3((F.nunits + 7) / 8);
-        block = dim3(512);
-        lds = lds48_scene_bytes(s);
-    } else {
-        grid = dim3((F.nunits + 3) / 4);
-        block = dim3(256);
-        lds = stack_bytes(s);
-    }
+    const dim3 grid((F.nunits + 3) / 4), block(256);
+    const size_t lds = stack_bytes(s);
     if (wavefront) {
-        r->host_cost.clear();   // no tile costs are measured for wavefront frames
-        int rc = launch_pt_frame(r, F, s->view, tex, st);
+        // per-tile cost map of a path-traced parameter set (rt_renderer_tile_costs, the multi-GPU
+        // deal's input): each tile's level-0 wave cycles -- its camera rays, their shading and
+        // NEE, summed over the samples -- recorded on the set's first frame, read on its second
+        // (one device synchronisation per set); the bounce levels follow the camera level's
+        // hits, so a sky tile is cheap at every level.  No tile order is built from it.
+        uint32_t *rec_cost = nullptr;
+        if (s->tile_order) {
+            const uint64_t pkey = param_key(r, F, cam, p);
+            const uint32_t n = F.ntiles_local;
+            if (pkey != r->order_key || n != r->order_n) {
+                r->order_key = pkey;
+                r->order_state = 0;
+                r->host_cost.clear();
+                if (n != r->order_n) {
+                    HIP_TRY(hipDeviceSynchronize());                             // frames may still read them
+                    if (r->d_order) HIP_TRY(hipFree(r->d_order));
+                    if (r->d_cost) HIP_TRY(hipFree(r->d_cost));
+                    r->d_order = r->d_cost = nullptr;
+                    r->order_n = 0;
+                    HIP_TRY(hipMalloc(&r->d_order, 3u * n * sizeof(uint32_t)));
+                    HIP_TRY(hipMalloc(&r->d_cost, 2u * n * sizeof(uint32_t)));
+                    r->order_n = n;
+                }
+            }
+            if (r->order_state == 0) {
+                if (!r->cost_ev) HIP_TRY(hipEventCreateWithFlags(&r->cost_ev, hipEventDisableTiming | hipEventReleaseToDevice));
+                HIP_TRY(hipMemsetAsync(r->d_cost, 0, n * sizeof(uint32_t), st));
+                HIP_TRY(hipEventRecord(r->cost_ev, st));
+                rec_cost = r->d_cost;
+                r->order_state = 1;
+            } else if (r->order_state == 1) {
+                HIP_TRY(hipDeviceSynchronize());                                 // the recording frame is done
+                r->host_cost.resize(n);
+                HIP_TRY(hipMemcpy(r->host_cost.data(), r->d_cost, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+                r->order_state = 3;                                              // costs held, no order
+            }
+        }
+        int rc = launch_pt_frame(r, F, s->view, tex, st, rec_cost);
         if (rc != RT_OK) return rc;
         r->primary += frame_pixels(r, F, shard, nshards, tiles_x, ntiles) * p->spp;
         r->frames += 1;
         return RT_OK;
     }
-    FrameLaunch L{mode, md, tex, lds_kind, grid, block, lds, st};
+    FrameLaunch L{mode, md, tex, grid, block, lds, st};
     SceneView view = s->view;
+    view.walk_stats = r->d_counters;
+    view.walk_check = r->walk_check;
     const uint64_t pkey = param_key(r, F, cam, p);
     bool gate_open = false;
     if (int rc = tune_gate(r, pkey, st, gate_open); rc != RT_OK) return rc;
     // camera-ray walk (only the global-node primary+shadow kernel has both)
-    const bool walk_kernel = mode == RT_MODE_PATH && md == 1 && lds_kind == 0 && !s->ext;
+    const bool walk_kernel = mode == RT_MODE_PATH && md == 1 && !s->ext;
     int walk_ev0 = -1, walk_ev1 = -1;   // tev recorded before / after this launch
     int cost_map = -1;                  // this frame records the tile costs under walk 0 / 1
     bool walk_decided = false;
+    // the walk's timed groups (lane, wave, wave, lane) must all run on one parameter set's
+    // frames: a set change in the middle (a multi-GPU deal switch, a camera move) restarts them
+    if (walk_kernel && s->walk == RT_WALK_AUTO && r->tune >= 1 && r->tune < kTuneDecide && pkey != r->tune_key)
+        r->tune = 0;
+    if (r->tune == 0) r->tune_key = pkey;
     const bool walk_pending = walk_kernel && s->walk == RT_WALK_AUTO && r->tune < kTuneDone;
     if (walk_kernel) {
         if (s->walk == RT_WALK_WAVE) view.wave_primary = 1;
@@ -1314,11 +1236,11 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     int split_ev0 = -1, split_ev1 = -1;   // sev recorded before / after this launch
     if (s->tile_order) {
         // half-tile units: primary+shadow frames of the global-node kernel, whole-tile units only
-        const bool split_ok = mode == RT_MODE_PATH && md == 1 && lds_kind == 0 && F.nchunks <= 1;
+        const bool split_ok = mode == RT_MODE_PATH && md == 1 && F.nchunks <= 1;
         const int rc = tile_order_step(r, F, pkey, cost_map >= 0 ? cost_map : walk_decided ? 2 : walk_pending ? 3 : -1,
                                        split_ok, gate_open, split_ev0, split_ev1);
         if (rc != RT_OK) return rc;
-        if (lds_kind == 0) L.grid = dim3((F.nunits + 3) / 4);
+        L.grid = dim3((F.nunits + 3) / 4);
     }
     // Overlapped primary+shadow frames: each pixel's accumulator update has to follow the
     // previous frame's, but its traversal does not.  Once the frame is in its steady state
@@ -1344,7 +1266,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     const uint64_t ps_bytes = (uint64_t)p->spp * F.ntiles_local * 64u * 16u;
     // (sample-split frames -- a multi-GPU rank's shard at spp N -- store their samples anyway;
     // overlapped, they go to the result buffers instead of d_samples)
-    const bool ps_ok = s->ps_pipeline != 0 && mode == RT_MODE_PATH && md == 1 && lds_kind == 0 &&
+    const bool ps_ok = s->ps_pipeline != 0 && mode == RT_MODE_PATH && md == 1 &&
                        split_ev0 < 0 && split_ev1 < 0 && r->split_phase < 0 && !F.tile_cost && !walk_pending &&
                        ps_bytes <= (2ull << 30);
     // frames in flight for this frame: 0 = serial, else 2..6 renderer streams
@@ -1486,33 +1408,29 @@ int rt::renderer_accumulator(rt_renderer *r, void **acc_dev, size_t *bytes) {
     return RT_OK;
 }
 
-static int acc_tiles(rt_renderer *r, const uint32_t *tiles, uint32_t n, void *buf, void *stream, int unpack) {
-    if (!r || (n && (!tiles || !buf))) return fail(RT_ERR_INVALID, "null argument");
+static int acc_tiles(rt_renderer *r, const uint32_t *d_tiles, uint32_t n, void *buf, void *stream, int unpack) {
+    if (!r || (n && (!d_tiles || !buf))) return fail(RT_ERR_INVALID, "null argument");
     if (n == 0) return RT_OK;
     HIP_TRY(hipSetDevice(r->scene->device));
-    const uint32_t tiles_x = (r->W + 7) / 8, ntiles = tiles_x * ((r->H + 7) / 8);
-    for (uint32_t i = 0; i < n; ++i)
-        if (tiles[i] >= ntiles) return fail(RT_ERR_INVALID, "tile index out of range");
-    uint32_t *d_tiles = nullptr;   // one-time operations: a private copy of the list
-    HIP_TRY(hipMalloc(&d_tiles, sizeof(uint32_t) * n));
-    hipError_t e = hipMemcpy(d_tiles, tiles, sizeof(uint32_t) * n, hipMemcpyHostToDevice);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_acc_tiles, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, r->d_acc,
-                           static_cast<float4 *>(buf), d_tiles, n, tiles_x, r->W, r->H, unpack);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
-    (void)hipFree(d_tiles);
-    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("accumulator tiles: ") + hipGetErrorString(e));
+    const uint32_t tiles_x = (r->W + 7) / 8;
+    hipLaunchKernelGGL(k_acc_tiles, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, r->d_acc,
+                       static_cast<float4 *>(buf), d_tiles, n, tiles_x, r->W, r->H, unpack);
+    HIP_TRY(hipGetLastError());
     return RT_OK;
 }
 
-int rt::accumulator_pack(rt_renderer *r, const uint32_t *tiles, uint32_t n, void *buf_dev, void *stream) {
-    return acc_tiles(r, tiles, n, buf_dev, stream, 0);
+int rt::accumulator_pack(rt_renderer *r, const uint32_t *tiles_dev, uint32_t n, void *buf_dev, void *stream) {
+    return acc_tiles(r, tiles_dev, n, buf_dev, stream, 0);
 }
 
-int rt::accumulator_unpack(rt_renderer *r, const uint32_t *tiles, uint32_t n, const void *buf_dev, void *stream) {
-    return acc_tiles(r, tiles, n, const_cast<void *>(buf_dev), stream, 1);
+int rt::accumulator_unpack(rt_renderer *r, const uint32_t *tiles_dev, uint32_t n, const void *buf_dev, void *stream) {
+    return acc_tiles(r, tiles_dev, n, const_cast<void *>(buf_dev), stream, 1);
+}
+
+int rt::render_shard_tiles_keyed(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, const uint32_t *tiles,
+                                 uint32_t n, uint64_t key, uint32_t *out_dev, void *stream) {
+    if (!r || (n && !tiles)) return fail(RT_ERR_INVALID, "render_shard_tiles_keyed: null argument");
+    return launch_render(r, cam, p, 0, 1, out_dev, 1, stream, tiles ? tiles : reinterpret_cast<const uint32_t *>(r), n, key);
 }
 
 int rt::renderer_geometry(const rt_renderer *r, uint32_t *W, uint32_t *H, int *device) {
@@ -1774,6 +1692,7 @@ int rt_renderer_destroy(rt_renderer *r) {
     for (auto &e : r->gate_ev)
         if (e) (void)hipEventDestroy(e);
     if (r->ps_join) (void)hipEventDestroy(r->ps_join);
+    if (r->cost_ev) (void)hipEventDestroy(r->cost_ev);
     for (int b = 0; b < kPsMaxDepth + 1; ++b) {
         if (r->ps_res[b]) (void)hipFree(r->ps_res[b]);
         if (r->ps_fin[b]) (void)hipEventDestroy(r->ps_fin[b]);
@@ -1879,6 +1798,29 @@ int rt_renderer_counters(rt_renderer *r, rt_counters *out) {
     return RT_OK;
 }
 
+int rt_renderer_set_walk_check(rt_renderer *r, int level) {
+    if (!r || level < RT_WALK_CHECK_OFF || level > RT_WALK_CHECK_VERIFY)
+        return fail(RT_ERR_INVALID, "rt_renderer_set_walk_check: bad argument");
+    r->walk_check = level;
+    return RT_OK;
+}
+
+int rt_renderer_walk_stats(rt_renderer *r, uint64_t out[4]) {
+    if (!r || !out) return fail(RT_ERR_INVALID, "rt_renderer_walk_stats: null argument");
+    HIP_TRY(hipSetDevice(r->scene->device));
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<unsigned long long> c((size_t)kCounterSlots * 8);
+    HIP_TRY(hipMemcpy(c.data(), r->d_counters, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 4; ++i) out[i] = 0;
+    for (uint32_t k = 0; k < kCounterSlots; ++k) {
+        out[0] += c[(size_t)k * 8 + 4];   // camera rays walked
+        out[1] += c[(size_t)k * 8 + 2];   // boxes entered through the margin
+        out[2] += c[(size_t)k * 8 + 3];   // lanes re-traced (tie / odd)
+        out[3] += c[(size_t)k * 8 + 5];   // verify: walk result differed
+    }
+    return RT_OK;
+}
+
 int rt_renderer_overlap(const rt_renderer *r, int *state, float ms[4]) {
     if (!r || !state) return fail(RT_ERR_INVALID, "rt_renderer_overlap: null argument");
     int depth = 0;
@@ -1966,9 +1908,6 @@ const char *rt_frame_kernel_name(const rt_renderer *r, const rt_frame_params *p)
     const rt_scene *s = r->scene;
     if (p->mode == RT_MODE_PATH && p->depth >= 2 && s->pt_wavefront) return "k_pt_level";
     const int md = max_depth_class(p->depth);
-    const int lds_kind = lds_kind_for(s, (int)p->mode, md);
-    if (lds_kind == 48) return "k_render_lds48<1>";
-    if (lds_kind == 64) return "k_render_lds<1>";
     static const char *names[3][4] = {
         {"k_render<path,1>", "k_render<path,4>", "k_render<path,10>", "k_render<path,32>"},
         {"k_render<whitted,1>", "k_render<whitted,1>", "k_render<whitted,1>", "k_render<whitted,1>"},

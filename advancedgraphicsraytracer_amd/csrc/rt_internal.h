@@ -46,12 +46,17 @@ int build_sbvh(const rt_prim *prims, const float *transforms, uint32_t n, Bvh &o
 // frame size and device of a renderer (rt_multi.cpp)
 int renderer_geometry(const rt_renderer *r, uint32_t *W, uint32_t *H, int *device);
 // the renderer's device accumulator (W*H float4 = 16 B each); and the accumulator values of
-// the listed 8x8 tiles packed as [i][64] float4 into buf_dev / written back from it (pixels
-// outside the frame: 0 / skipped), on `stream` -- rt_multi.cpp moves a pixel's running average
-// to its new rank when a multi-GPU deal changes owners
+// the 8x8 tiles listed in DEVICE memory (tiles_dev) packed as [i][64] float4 into buf_dev /
+// written back from it (pixels outside the frame: 0 / skipped), in stream order on `stream`
+// with no host synchronisation -- rt_multi.cpp moves a pixel's running average to its new rank
+// when a multi-GPU deal changes owners
 int renderer_accumulator(rt_renderer *r, void **acc_dev, size_t *bytes);
-int accumulator_pack(rt_renderer *r, const uint32_t *tiles, uint32_t n, void *buf_dev, void *stream);
-int accumulator_unpack(rt_renderer *r, const uint32_t *tiles, uint32_t n, const void *buf_dev, void *stream);
+int accumulator_pack(rt_renderer *r, const uint32_t *tiles_dev, uint32_t n, void *buf_dev, void *stream);
+int accumulator_unpack(rt_renderer *r, const uint32_t *tiles_dev, uint32_t n, const void *buf_dev, void *stream);
+// rt_render_shard_tiles with the caller's identity of the tile list (key != 0): the multi-GPU
+// frame renders the same deal frame after frame and the renderer then skips hashing the list
+int render_shard_tiles_keyed(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, const uint32_t *tiles,
+                             uint32_t n, uint64_t key, uint32_t *out_dev, void *stream);
 
 // SURVEY.md 8(d) scenes as descriptions
 struct SceneSource {

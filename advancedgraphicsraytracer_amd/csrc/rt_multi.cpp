@@ -19,8 +19,10 @@
 #include <string>
 #include <type_traits>
 #include <array>
+#include <memory>
 #include <vector>
 
+#include "rt_dev_types.h"
 #include "rt_internal.h"
 
 using namespace rt;
@@ -104,22 +106,35 @@ int comm_fail(const Rccl &R, ncclResult_t e, const char *what) {
 
 }  // namespace
 
-// One communicator + the per-renderer exchange buffers (double-buffered for the pipelined mode).
-// A frame is rendered under a deal (which rank owns which 8x8 tiles): the interleaved deal
-// t % world == rank, or with RT_MULTI_BALANCED -- from the kDealAfter-th frame of a parameter
-// set on -- the cost-balanced compact deal of rt_tile_deal, built once per parameter set from
-// the ranks' measured tile costs (one exchange: costs to rank 0, the deal back to every rank).
+// A deal: which rank renders which 8x8 tiles (the rt_tile_deal layout: rank k owns
+// tiles[off[k] .. off[k+1])).  The interleaved deal t % world == rank has id 0; cost-balanced
+// deals (RT_MULTI_BALANCED) get ids 1, 2, ... in the order they are built.  Rank 0 keeps a
+// device map for the assembly of a balanced deal: (shard << 24 | local index) per global tile.
 struct Deal {
-    std::vector<uint32_t> tiles, off;      // rt_tile_deal layout
+    std::vector<uint32_t> tiles, off;
+    std::vector<uint8_t> owner;            // rank of every global tile
+    uint64_t id = 0;
+    uint32_t *d_where = nullptr;
+    int device = 0;
     uint32_t count(int k) const { return off[k + 1] - off[k]; }
+    ~Deal() {
+        if (d_where) {
+            (void)hipSetDevice(device);
+            (void)hipFree(d_where);
+        }
+    }
 };
+using DealP = std::shared_ptr<const Deal>;
 
+// One communicator + the per-renderer exchange buffers (double-buffered for the pipelined mode).
+// Every collective after set-up -- the per-frame gathers, the cost exchange and the accumulator
+// moves of a deal change -- runs on the communicator's own stream, so the communicator's
+// operations are serialised in issue order on every rank whatever streams the caller uses.
 struct rt_comm {
     ncclComm_t comm = nullptr;
     bool owned = false;
     int rank = 0, world = 1, device = 0;
-    hipStream_t comm_stream = nullptr;     // pipelined gathers run here, beside the next render
-    hipStream_t setup_stream = nullptr;    // the one-time deal exchange
+    hipStream_t comm_stream = nullptr;
     const rt_renderer *renderer = nullptr; // buffers below belong to this renderer's frame size
     uint32_t W = 0, H = 0, ntiles = 0;
     uint32_t stride = 0;                   // packed pixels per shard slot (room for any deal)
@@ -129,19 +144,27 @@ struct rt_comm {
     hipEvent_t ev_asm[2] = {nullptr, nullptr};   // rank 0, pipelined: frame assembled (comm stream)
     hipEvent_t ev_caller = nullptr;        // rank 0, pipelined: the caller's stream at the call, so the
                                            // unshuffle into rgb8_dev follows the caller's reads of it
+    hipEvent_t ev_mig[2] = {nullptr, nullptr};   // accumulator move: caller -> comm stream -> caller
     int slot = 0;
     int pending = -1;                      // slot whose gather is in flight (pipelined mode)
-    int slot_deal[2] = {0, 0};             // the deal a slot's frame was rendered under: 0 interleaved, 1 balanced
+    DealP slot_deal[2];                    // the deal a slot's frame was rendered under
     uint64_t frames = 0;
-    Deal interleaved, balanced;
-    Deal last_balanced;                    // the balanced deal the last balanced frame used
-    int last_deal = -1;                    // deal of the previous frame (-1 none yet)
-    uint64_t deal_version = 0, last_version = 0;   // balanced deals built / the one last used
-    uint64_t deal_key = 0;                 // parameter set the balanced deal belongs to
-    uint32_t key_calls = 0;                // frames of that parameter set so far
-    bool deal_on = false;
-    bool deal_moot = false;                // no costs measured (path-traced frames): keep interleaving
-    uint32_t *d_setup = nullptr;           // staging of the exchange
+    DealP interleaved, cur;                // cur: the deal frames are rendered under now
+    uint64_t deals_built = 0;              // balanced deals built (their ids)
+    // RT_MULTI_BALANCED: a parameter set (camera, size, spp, depth, mode) tries to balance the
+    // deal on its kDealAfter-th frame, then after 2x, 4x, ... as many frames until every rank has
+    // measured tile costs (a renderer records them once its own timed choices are done), and not
+    // again until the parameters change.  The deal in use is kept across parameter changes.
+    uint64_t pkey = 0;
+    uint32_t pcalls = 0, next_try = 0;
+    bool settled = false;
+    // staging, allocated with the renderer binding (nothing is allocated between collectives)
+    uint32_t *d_setup = nullptr;           // cost exchange: world blocks of (2 + ntiles) words
+    void *d_mig_send = nullptr, *d_mig_recv = nullptr;   // accumulator moves: ntiles x 64 float4 each
+    uint32_t *d_mig_list = nullptr;        // ... their tile lists (2 x ntiles)
+    uint32_t *h_mig_list = nullptr;        // pinned host staging of those lists
+    bool mig_pending = false;              // ev_mig[1] marks a move whose list upload may still run
+    uint64_t n_exchanges = 0, n_migrations = 0, n_mig_skipped = 0;
     // RT_MULTI_TIMING: per frame (render start, render end, gather end) events, summed by rt_comm_timing
     std::vector<std::array<hipEvent_t, 3>> tev;
     size_t tev_used = 0;
@@ -149,8 +172,8 @@ struct rt_comm {
 
 namespace {
 
-// frames of a parameter set rendered under the interleaved deal before the balanced one is built:
-// the renderer records its tile costs and sorts them within its first four frames
+// frames of a parameter set rendered before its first balancing attempt: the renderer records
+// its tile costs within its first frames unless a timed camera walk holds them back
 constexpr uint32_t kDealAfter = 6;
 
 void free_buffers(rt_comm *c) {
@@ -158,16 +181,45 @@ void free_buffers(rt_comm *c) {
         if (c->tiles[k]) (void)hipFree(c->tiles[k]);
         if (c->gathered[k]) (void)hipFree(c->gathered[k]);
         c->tiles[k] = c->gathered[k] = nullptr;
+        c->slot_deal[k].reset();
     }
-    if (c->d_setup) (void)hipFree(c->d_setup);
-    c->d_setup = nullptr;
+    for (void *p : {(void *)c->d_setup, c->d_mig_send, c->d_mig_recv, (void *)c->d_mig_list})
+        if (p) (void)hipFree(p);
+    if (c->h_mig_list) (void)hipHostFree(c->h_mig_list);
+    c->h_mig_list = nullptr;
+    c->mig_pending = false;
+    c->d_setup = c->d_mig_list = nullptr;
+    c->d_mig_send = c->d_mig_recv = nullptr;
+    c->interleaved.reset();
+    c->cur.reset();
     c->renderer = nullptr;
     c->stride = 0;
     c->pending = -1;
-    c->deal_on = false;
-    c->deal_key = 0;
-    c->key_calls = 0;
-    c->last_deal = -1;
+    c->pkey = 0;
+    c->pcalls = 0;
+    c->settled = false;
+}
+
+// a deal from its tile lists; rank 0 uploads the assembly map of a balanced one
+int make_deal(rt_comm *c, std::vector<uint32_t> tiles, std::vector<uint32_t> off, uint64_t id, DealP &out) {
+    auto d = std::make_shared<Deal>();
+    d->tiles = std::move(tiles);
+    d->off = std::move(off);
+    d->id = id;
+    d->device = c->device;
+    d->owner.assign(c->ntiles, 0);
+    std::vector<uint32_t> where(c->ntiles, 0);
+    for (int k = 0; k < c->world; ++k)
+        for (uint32_t i = d->off[k]; i < d->off[k + 1]; ++i) {
+            d->owner[d->tiles[i]] = (uint8_t)k;
+            where[d->tiles[i]] = ((uint32_t)k << 24) | (i - d->off[k]);
+        }
+    if (c->rank == 0 && id != 0) {
+        HIP_TRY(hipMalloc(&d->d_where, sizeof(uint32_t) * c->ntiles));
+        HIP_TRY(hipMemcpy(d->d_where, where.data(), sizeof(uint32_t) * c->ntiles, hipMemcpyHostToDevice));
+    }
+    out = d;
+    return RT_OK;
 }
 
 int bind_renderer(rt_comm *c, rt_renderer *r) {
@@ -186,19 +238,25 @@ int bind_renderer(rt_comm *c, rt_renderer *r) {
         if (c->rank == 0) HIP_TRY(hipMalloc(&c->gathered[k], sizeof(uint32_t) * (size_t)stride * c->world));
         else HIP_TRY(hipMalloc(&c->tiles[k], sizeof(uint32_t) * (size_t)stride));
     }
-    HIP_TRY(hipMalloc(&c->d_setup, sizeof(uint32_t) * ((size_t)ntiles + c->world + 1)));
-    Deal &d = c->interleaved;   // t % world == rank, in tile order (rt_render_shard's packing)
-    d.tiles.clear();
-    d.off.assign(1, 0);
-    for (int k = 0; k < c->world; ++k) {
-        for (uint32_t t = (uint32_t)k; t < ntiles; t += (uint32_t)c->world) d.tiles.push_back(t);
-        d.off.push_back((uint32_t)d.tiles.size());
+    if (c->world > 1) {
+        HIP_TRY(hipMalloc(&c->d_setup, sizeof(uint32_t) * ((size_t)ntiles + 2) * c->world));
+        HIP_TRY(hipMalloc(&c->d_mig_send, (size_t)stride * 16u));
+        HIP_TRY(hipMalloc(&c->d_mig_recv, (size_t)stride * 16u));
+        HIP_TRY(hipMalloc(&c->d_mig_list, sizeof(uint32_t) * 2u * ntiles));
+        HIP_TRY(hipHostMalloc(&c->h_mig_list, sizeof(uint32_t) * 2u * ntiles, hipHostMallocDefault));
     }
-    c->renderer = r;
     c->W = W;
     c->H = H;
     c->ntiles = ntiles;
     c->stride = stride;
+    std::vector<uint32_t> tl, off(1, 0);   // t % world == rank, in tile order (rt_render_shard's packing)
+    for (int k = 0; k < c->world; ++k) {
+        for (uint32_t t = (uint32_t)k; t < ntiles; t += (uint32_t)c->world) tl.push_back(t);
+        off.push_back((uint32_t)tl.size());
+    }
+    if ((rc = make_deal(c, std::move(tl), std::move(off), 0, c->interleaved)) != RT_OK) return rc;
+    c->cur = c->interleaved;
+    c->renderer = r;
     c->slot = 0;
     return RT_OK;
 }
@@ -238,11 +296,15 @@ unsigned sync_event_flags() {
     return hipEventDisableTiming | (e && std::strcmp(e, "system") == 0 ? 0u : (unsigned)hipEventReleaseToDevice);
 }
 
-int assemble(rt_comm *c, rt_renderer *r, int k, uint32_t *rgb8, hipStream_t st) {
+// rank 0: slot k's gathered shards -> the row-major frame, under the deal that slot was rendered with
+int assemble(rt_comm *c, int k, uint32_t *rgb8, hipStream_t st) {
     if (c->rank != 0) return RT_OK;
     if (!rgb8) return fail(RT_ERR_INVALID, "rt_render_frame_multi: rank 0 needs an output frame");
-    const Deal &d = c->slot_deal[k] ? c->balanced : c->interleaved;
-    return rt_assemble_tiles(r, c->gathered[k], c->stride, d.tiles.data(), d.off.data(), (uint32_t)c->world, rgb8, st);
+    const Deal &d = *c->slot_deal[k];
+    launch_assemble(c->gathered[k], c->stride, (uint32_t)c->world, d.id ? d.d_where : nullptr, (c->W + 7) / 8,
+                    c->ntiles, c->W, c->H, rgb8, st);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
 }
 
 uint64_t params_key(const rt_camera *cam, const rt_frame_params *p) {
@@ -257,132 +319,117 @@ uint64_t params_key(const rt_camera *cam, const rt_frame_params *p) {
     return h;
 }
 
-// The one-time exchange behind the balanced deal (every rank, the same call): each rank's
-// measured costs of its interleaved tiles to rank 0, rank 0 builds rt_tile_deal over the whole
-// frame (equal costs when any rank has none, e.g. path-traced frames), the deal back to every
-// rank.  Blocking: it runs once per parameter set.
-int exchange_deal(rt_comm *c, rt_renderer *r) {
+// One balancing attempt (every rank, the same call): an all-gather of the ranks' measured tile
+// costs under the current deal -- each rank sends one block [status, count, costs] to every
+// peer inside one group -- then every rank builds the same rt_tile_deal over the whole frame
+// (deterministic host code on identical inputs).  The status words make the outcome collective:
+// a rank that could not read its costs fails the call on every rank, and the deal changes only
+// when every rank measured its tiles (`complete`).  Blocking: O(log frames) calls per parameter set.
+int rebalance(rt_comm *c, rt_renderer *r, DealP &next, bool &complete) {
     const Rccl &R = rccl();
-    if (!c->setup_stream) HIP_TRY(hipStreamCreateWithFlags(&c->setup_stream, hipStreamNonBlocking));
-    const Deal &il = c->interleaved;
-    const uint32_t mine = il.count(c->rank);
-    std::vector<uint32_t> cost(mine, 0u);
+    const Deal &cur = *c->cur;
+    uint32_t most = 0;
+    for (int k = 0; k < c->world; ++k) most = std::max(most, cur.count(k));
+    const uint32_t B = 2 + most;
+    const uint32_t mine = cur.count(c->rank);
+    std::vector<uint32_t> block(B, 0u);
     uint32_t have = 0;
-    int rc = rt_renderer_tile_costs(r, cost.data(), mine, &have);
-    if (rc != RT_OK) return rc;
-    if (have != mine) std::fill(cost.begin(), cost.end(), 0u);   // none recorded: 0 = "no costs"
-    hipStream_t st = c->setup_stream;
-    std::vector<uint32_t> all(c->ntiles, 0u);
-    if (c->rank == 0) {
-        std::copy(cost.begin(), cost.end(), all.begin());
-        if (c->world > 1) {
-            NCCL_TRY(R, R.group_start(), "ncclGroupStart");
-            for (int peer = 1; peer < c->world; ++peer)
-                NCCL_TRY(R, R.recv(c->d_setup + il.off[peer], sizeof(uint32_t) * il.count(peer), ncclUint8, peer, c->comm, st), "ncclRecv");
-            NCCL_TRY(R, R.group_end(), "ncclGroupEnd");
-            HIP_TRY(hipStreamSynchronize(st));
-            HIP_TRY(hipMemcpy(all.data() + il.off[1], c->d_setup + il.off[1], sizeof(uint32_t) * (c->ntiles - il.off[1]),
-                              hipMemcpyDeviceToHost));
+    const int lrc = rt_renderer_tile_costs(r, block.data() + 2, mine, &have);
+    bool any = mine == 0;
+    for (uint32_t i = 0; i < mine && lrc == RT_OK && have == mine; ++i) any = any || block[2 + i] != 0;
+    block[0] = (lrc != RT_OK ? 2u : 0u) | (lrc == RT_OK && have == mine && any ? 1u : 0u);
+    block[1] = mine;
+    hipStream_t st = c->comm_stream;
+    uint32_t *own = c->d_setup + (size_t)c->rank * B;
+    HIP_TRY(hipMemcpyAsync(own, block.data(), sizeof(uint32_t) * B, hipMemcpyHostToDevice, st));
+    NCCL_TRY(R, R.group_start(), "ncclGroupStart");
+    for (int q = 0; q < c->world; ++q) {
+        if (q == c->rank) continue;
+        ncclResult_t e = R.send(own, sizeof(uint32_t) * B, ncclUint8, q, c->comm, st);
+        if (e == ncclSuccess) e = R.recv(c->d_setup + (size_t)q * B, sizeof(uint32_t) * B, ncclUint8, q, c->comm, st);
+        if (e != ncclSuccess) {
+            (void)R.group_end();
+            return comm_fail(R, e, "cost exchange");
         }
-        // local order -> global tile; a rank without costs (zeros) makes the deal count-balanced
-        std::vector<uint32_t> global(c->ntiles, 0u);
-        bool complete = true;
-        for (int k = 0; k < c->world; ++k) {
-            bool any = false;
-            for (uint32_t i = il.off[k]; i < il.off[k + 1]; ++i) {
-                global[il.tiles[i]] = all[i];
-                any = any || all[i] != 0;
-            }
-            complete = complete && (any || il.count(k) == 0);
-        }
-        // without measured costs (path-traced frames record none) equal-count regions measured
-        // worse than interleaving (CFG5-sub 1/4 shards 3.36 vs 2.54 ms): keep the interleaved deal
-        Deal &d = c->balanced;
-        if (complete) {
-            d.tiles.assign(c->ntiles, 0u);
-            d.off.assign((size_t)c->world + 1, 0u);
-            if ((rc = rt_tile_deal(c->W, c->H, global.data(), (uint32_t)c->world, d.tiles.data(), d.off.data())) != RT_OK)
-                return rc;
-        } else {
-            d = c->interleaved;
-        }
-        if (c->world > 1) {
-            std::vector<uint32_t> msg(d.off);
-            msg.insert(msg.end(), d.tiles.begin(), d.tiles.end());
-            HIP_TRY(hipMemcpy(c->d_setup, msg.data(), sizeof(uint32_t) * msg.size(), hipMemcpyHostToDevice));
-            NCCL_TRY(R, R.group_start(), "ncclGroupStart");
-            for (int peer = 1; peer < c->world; ++peer)
-                NCCL_TRY(R, R.send(c->d_setup, sizeof(uint32_t) * msg.size(), ncclUint8, peer, c->comm, st), "ncclSend");
-            NCCL_TRY(R, R.group_end(), "ncclGroupEnd");
-            HIP_TRY(hipStreamSynchronize(st));
-        }
-    } else {
-        HIP_TRY(hipMemcpy(c->d_setup, cost.data(), sizeof(uint32_t) * mine, hipMemcpyHostToDevice));
-        NCCL_TRY(R, R.send(c->d_setup, sizeof(uint32_t) * mine, ncclUint8, 0, c->comm, st), "ncclSend");
-        HIP_TRY(hipStreamSynchronize(st));
-        const size_t words = (size_t)c->world + 1 + c->ntiles;
-        NCCL_TRY(R, R.recv(c->d_setup, sizeof(uint32_t) * words, ncclUint8, 0, c->comm, st), "ncclRecv");
-        HIP_TRY(hipStreamSynchronize(st));
-        std::vector<uint32_t> msg(words);
-        HIP_TRY(hipMemcpy(msg.data(), c->d_setup, sizeof(uint32_t) * words, hipMemcpyDeviceToHost));
-        c->balanced.off.assign(msg.begin(), msg.begin() + c->world + 1);
-        c->balanced.tiles.assign(msg.begin() + c->world + 1, msg.end());
     }
-    c->deal_on = true;
-    c->deal_moot = c->balanced.tiles == c->interleaved.tiles && c->balanced.off == c->interleaved.off;
-    c->deal_version += 1;
-    return RT_OK;
+    NCCL_TRY(R, R.group_end(), "ncclGroupEnd");
+    std::vector<uint32_t> all((size_t)B * c->world);
+    HIP_TRY(hipMemcpyAsync(all.data(), c->d_setup, sizeof(uint32_t) * all.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    c->n_exchanges += 1;
+    if (lrc != RT_OK) return lrc;
+    complete = true;
+    for (int k = 0; k < c->world; ++k) {
+        const uint32_t status = all[(size_t)k * B];
+        if (status & 2u) return fail(RT_ERR_COMM, "rt_render_frame_multi: rank " + std::to_string(k) + " could not read its tile costs");
+        if (all[(size_t)k * B + 1] != cur.count(k)) return fail(RT_ERR_COMM, "rt_render_frame_multi: ranks disagree on the deal");
+        complete = complete && (status & 1u);
+    }
+    next = c->cur;
+    if (!complete) return RT_OK;   // e.g. a renderer still timing its camera walk: try again later
+    std::vector<uint32_t> global(c->ntiles, 0u);
+    for (int k = 0; k < c->world; ++k)
+        for (uint32_t i = 0; i < cur.count(k); ++i) global[cur.tiles[cur.off[k] + i]] = all[(size_t)k * B + 2 + i];
+    std::vector<uint32_t> tiles(c->ntiles), off((size_t)c->world + 1);
+    int rc = rt_tile_deal(c->W, c->H, global.data(), (uint32_t)c->world, tiles.data(), off.data());
+    if (rc != RT_OK) return rc;
+    if (tiles == cur.tiles && off == cur.off) return RT_OK;
+    return make_deal(c, std::move(tiles), std::move(off), ++c->deals_built, next);
 }
 
-// Tiles change owner between two frames (interleaved <-> balanced deal): a pixel's running
-// average (renderer.cpp:235-241) must go on from the frames its previous owner accumulated.
-// Every rank packs its accumulator values of the tiles it owned under the old deal, rank 0
-// writes them into its accumulator (now the whole frame's) and hands that to every rank.
-// Collective and blocking; once per deal switch.
-int migrate_accumulators(rt_comm *c, rt_renderer *r, const Deal &old) {
+// Tiles change owner between two frames: a pixel's running average (renderer.cpp:235-241) must
+// go on from the frames its previous owner accumulated.  Each rank sends the accumulator values
+// of every tile it owned under `from` and owns no longer straight to the tile's owner under
+// `to` (one group of point-to-point transfers, each pair's tiles in `from` order) and writes the
+// ones it receives into its accumulator.  In stream order: the caller's stream's earlier frames
+// have updated the accumulator before the pack, and its next frame renders after the unpack --
+// no host synchronisation, no whole-frame broadcast.  Frames that reset the accumulator skip it.
+int migrate(rt_comm *c, rt_renderer *r, const Deal &from, const Deal &to, hipStream_t st) {
     const Rccl &R = rccl();
-    if (!c->setup_stream) HIP_TRY(hipStreamCreateWithFlags(&c->setup_stream, hipStreamNonBlocking));
-    hipStream_t st = c->setup_stream;
-    HIP_TRY(hipDeviceSynchronize());   // every frame so far has updated its accumulator
-    void *acc = nullptr;
-    size_t bytes = 0;
-    int rc = renderer_accumulator(r, &acc, &bytes);
+    std::vector<uint32_t> L;
+    std::vector<uint32_t> send_off(c->world + 1, 0), recv_off(c->world + 1, 0);
+    for (int q = 0; q < c->world; ++q) {   // mine under `from`, q's under `to`
+        for (uint32_t i = from.off[c->rank]; i < from.off[c->rank + 1]; ++i)
+            if (q != c->rank && to.owner[from.tiles[i]] == q) L.push_back(from.tiles[i]);
+        send_off[q + 1] = (uint32_t)L.size();
+    }
+    const uint32_t nsend = (uint32_t)L.size();
+    for (int q = 0; q < c->world; ++q) {   // q's under `from`, mine under `to`
+        for (uint32_t i = from.off[q]; i < from.off[q + 1]; ++i)
+            if (q != c->rank && to.owner[from.tiles[i]] == c->rank) L.push_back(from.tiles[i]);
+        recv_off[q + 1] = (uint32_t)L.size() - nsend;
+    }
+    const uint32_t nrecv = (uint32_t)L.size() - nsend;
+    hipStream_t cs = c->comm_stream;
+    HIP_TRY(hipEventRecord(c->ev_mig[0], st));
+    HIP_TRY(hipStreamWaitEvent(cs, c->ev_mig[0], 0));
+    if (c->mig_pending) HIP_TRY(hipEventSynchronize(c->ev_mig[1]));   // the previous move read the staging
+    std::copy(L.begin(), L.end(), c->h_mig_list);
+    if (!L.empty()) HIP_TRY(hipMemcpyAsync(c->d_mig_list, c->h_mig_list, sizeof(uint32_t) * L.size(), hipMemcpyHostToDevice, cs));
+    int rc = accumulator_pack(r, c->d_mig_list, nsend, c->d_mig_send, cs);
     if (rc != RT_OK) return rc;
-    uint32_t most = 0;
-    for (int k = 0; k < c->world; ++k) most = std::max(most, old.count(k));
-    void *staging = nullptr;
-    HIP_TRY(hipMalloc(&staging, std::max<size_t>(16, (size_t)most * 64u * 16u)));
-    auto run = [&]() -> int {
-        if (c->rank == 0) {
-            for (int peer = 1; peer < c->world; ++peer) {
-                const uint32_t n = old.count(peer);
-                if (!n) continue;
-                NCCL_TRY(R, R.recv(staging, (size_t)n * 64u * 16u, ncclUint8, peer, c->comm, st), "ncclRecv");
-                HIP_TRY(hipStreamSynchronize(st));
-                int e = accumulator_unpack(r, old.tiles.data() + old.off[peer], n, staging, st);
-                if (e != RT_OK) return e;
-            }
-            NCCL_TRY(R, R.group_start(), "ncclGroupStart");
-            for (int peer = 1; peer < c->world; ++peer)
-                NCCL_TRY(R, R.send(acc, bytes, ncclUint8, peer, c->comm, st), "ncclSend");
-            NCCL_TRY(R, R.group_end(), "ncclGroupEnd");
-            HIP_TRY(hipStreamSynchronize(st));
-        } else {
-            const uint32_t n = old.count(c->rank);
-            if (n) {
-                int e = accumulator_pack(r, old.tiles.data() + old.off[c->rank], n, staging, st);
-                if (e != RT_OK) return e;
-                NCCL_TRY(R, R.send(staging, (size_t)n * 64u * 16u, ncclUint8, 0, c->comm, st), "ncclSend");
-                HIP_TRY(hipStreamSynchronize(st));
-            }
-            NCCL_TRY(R, R.recv(acc, bytes, ncclUint8, 0, c->comm, st), "ncclRecv");
-            HIP_TRY(hipStreamSynchronize(st));
+    const size_t tile_bytes = 64u * 16u;
+    char *sb = static_cast<char *>(c->d_mig_send), *rb = static_cast<char *>(c->d_mig_recv);
+    NCCL_TRY(R, R.group_start(), "ncclGroupStart");
+    for (int q = 0; q < c->world; ++q) {
+        if (q == c->rank) continue;
+        ncclResult_t e = ncclSuccess;
+        if (send_off[q + 1] > send_off[q])
+            e = R.send(sb + send_off[q] * tile_bytes, (send_off[q + 1] - send_off[q]) * tile_bytes, ncclUint8, q, c->comm, cs);
+        if (e == ncclSuccess && recv_off[q + 1] > recv_off[q])
+            e = R.recv(rb + recv_off[q] * tile_bytes, (recv_off[q + 1] - recv_off[q]) * tile_bytes, ncclUint8, q, c->comm, cs);
+        if (e != ncclSuccess) {
+            (void)R.group_end();
+            return comm_fail(R, e, "accumulator move");
         }
-        return RT_OK;
-    };
-    rc = run();
-    (void)hipFree(staging);
-    return rc;
+    }
+    NCCL_TRY(R, R.group_end(), "ncclGroupEnd");
+    if ((rc = accumulator_unpack(r, c->d_mig_list + nsend, nrecv, c->d_mig_recv, cs)) != RT_OK) return rc;
+    HIP_TRY(hipEventRecord(c->ev_mig[1], cs));
+    HIP_TRY(hipStreamWaitEvent(st, c->ev_mig[1], 0));
+    c->mig_pending = true;
+    c->n_migrations += 1;
+    return RT_OK;
 }
 
 }  // namespace
@@ -494,14 +541,30 @@ int rt_comm_destroy(rt_comm *c) {
         if (c->ev_render[k]) (void)hipEventDestroy(c->ev_render[k]);
         if (c->ev_gather[k]) (void)hipEventDestroy(c->ev_gather[k]);
         if (c->ev_asm[k]) (void)hipEventDestroy(c->ev_asm[k]);
+        if (c->ev_mig[k]) (void)hipEventDestroy(c->ev_mig[k]);
     }
     if (c->ev_caller) (void)hipEventDestroy(c->ev_caller);
     for (auto &e : c->tev)
         for (auto &x : e) (void)hipEventDestroy(x);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
-    if (c->setup_stream) (void)hipStreamDestroy(c->setup_stream);
     if (c->owned && c->comm) (void)rccl().comm_destroy(c->comm);
     delete c;
+    return RT_OK;
+}
+
+int rt_comm_deal_info(const rt_comm *c, int *balanced, uint32_t *ntiles, uint32_t *tile_list, uint64_t stats[4]) {
+    if (!c) return fail(RT_ERR_INVALID, "rt_comm_deal_info: null argument");
+    const bool bal = c->cur && c->cur->id != 0;
+    if (balanced) *balanced = bal ? 1 : 0;
+    const uint32_t n = c->cur ? c->cur->count(c->rank) : 0u;
+    if (ntiles) *ntiles = n;
+    if (tile_list && n) std::memcpy(tile_list, c->cur->tiles.data() + c->cur->off[c->rank], sizeof(uint32_t) * n);
+    if (stats) {
+        stats[0] = c->deals_built;
+        stats[1] = c->n_exchanges;
+        stats[2] = c->n_migrations;
+        stats[3] = c->n_mig_skipped;
+    }
     return RT_OK;
 }
 
@@ -518,47 +581,59 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
     if (c->rank == 0 && !rgb8_dev && (!pipelined || c->pending >= 0))
         return fail(RT_ERR_INVALID, "rt_render_frame_multi: rank 0 needs an output frame");
     HIP_TRY(hipSetDevice(c->device));
-    int rc = bind_renderer(c, r);
-    if (rc != RT_OK) return rc;
-    hipStream_t st = (hipStream_t)stream;
-    if (pipelined && !c->comm_stream) {
+    if (!c->comm_stream) {
         HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
         for (int j = 0; j < 2; ++j) {
             HIP_TRY(hipEventCreateWithFlags(&c->ev_render[j], sync_event_flags()));
             HIP_TRY(hipEventCreateWithFlags(&c->ev_gather[j], sync_event_flags()));
             HIP_TRY(hipEventCreateWithFlags(&c->ev_asm[j], sync_event_flags()));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_mig[j], sync_event_flags()));
         }
         HIP_TRY(hipEventCreateWithFlags(&c->ev_caller, sync_event_flags()));
     }
+    int rc = bind_renderer(c, r);
+    if (rc != RT_OK) return rc;
+    hipStream_t st = (hipStream_t)stream;
     // rank 0, pipelined: this call unshuffles the previous frame into rgb8_dev on the
     // communicator's stream; whatever the caller queued on its stream before this call (a copy
     // or display of the frame before) must be done with rgb8_dev first
     const bool assemble_prev = pipelined && c->rank == 0 && c->pending >= 0;
     if (assemble_prev) HIP_TRY(hipEventRecord(c->ev_caller, st));
-    // the deal of this frame: interleaved, or (RT_MULTI_BALANCED) the balanced deal of this
-    // parameter set, exchanged once on its kDealAfter-th frame
-    const uint64_t key = params_key(cam, p);
-    if (key != c->deal_key) {
-        c->deal_key = key;
-        c->key_calls = 0;
-        c->deal_on = false;
+    // the deal of this frame: the interleaved one, or with RT_MULTI_BALANCED the last deal
+    // balanced on measured tile costs -- kept across camera moves; each parameter set tries to
+    // rebalance on its kDealAfter-th frame (then 2x, 4x, ... until every rank has costs).  Every
+    // rank takes the same decisions: same frames, same parameters, same flags.
+    DealP next = c->cur;
+    if (c->world > 1) {
+        if (!(flags & RT_MULTI_BALANCED)) {
+            next = c->interleaved;
+        } else {
+            const uint64_t key = params_key(cam, p);
+            if (key != c->pkey) {
+                c->pkey = key;
+                c->pcalls = 0;
+                c->next_try = kDealAfter;
+                c->settled = false;
+            }
+            if (!c->settled && c->pcalls == c->next_try) {
+                bool complete = false;
+                if ((rc = rebalance(c, r, next, complete)) != RT_OK) return rc;
+                if (complete) c->settled = true;
+                else c->next_try = c->next_try < (1u << 30) ? 2u * c->next_try : c->next_try;
+            }
+            c->pcalls += 1;
+        }
+        if (next != c->cur) {
+            // tiles change owner: their running averages move along, unless this frame starts the
+            // accumulation over (the reference resets it on camera motion, renderer.cpp:204-208, 237)
+            if (p->reset) c->n_mig_skipped += 1;
+            else if ((rc = migrate(c, r, *c->cur, *next, st)) != RT_OK) return rc;
+            c->cur = next;
+        }
     }
-    if ((flags & RT_MULTI_BALANCED) && !c->deal_on && c->key_calls >= kDealAfter && (rc = exchange_deal(c, r)) != RT_OK)
-        return rc;
-    c->key_calls += 1;
-    const bool use_balanced = (flags & RT_MULTI_BALANCED) && c->deal_on && !c->deal_moot;
-    const Deal &deal = use_balanced ? c->balanced : c->interleaved;
-    const int deal_id = use_balanced ? 1 : 0;
-    if (c->world > 1 && c->last_deal >= 0 && (c->last_deal != deal_id || (deal_id == 1 && c->last_version != c->deal_version))) {
-        // the frames before were rendered under another deal: move the accumulators first
-        // (pending pipelined work is finished by the device-wide sync inside)
-        if ((rc = migrate_accumulators(c, r, c->last_deal == 1 ? c->last_balanced : c->interleaved)) != RT_OK) return rc;
-    }
-    if (deal_id == 1 && c->last_version != c->deal_version) c->last_balanced = c->balanced;
-    c->last_deal = deal_id;
-    c->last_version = c->deal_version;
+    const Deal &deal = *c->cur;
     const int k = c->slot;
-    c->slot_deal[k] = deal_id;
+    c->slot_deal[k] = c->cur;
     uint32_t *mine = c->rank == 0 ? c->gathered[k] : c->tiles[k];
     std::array<hipEvent_t, 3> *tv = nullptr;
     if (flags & RT_MULTI_TIMING) {
@@ -570,31 +645,37 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
         tv = &c->tev[c->tev_used++];
         HIP_TRY(hipEventRecord((*tv)[0], st));
     }
-    if (use_balanced)
-        rc = rt_render_shard_tiles(r, cam, p, deal.tiles.data() + deal.off[c->rank], deal.count(c->rank), mine, st);
-    else
+    if (deal.id != 0) {
+        // the renderer keys its tile map by (communicator, deal, rank) instead of hashing the list
+        const uint64_t key = ((uint64_t)(uintptr_t)c * 0x100000001b3ull) ^ (deal.id << 8) ^ (uint64_t)c->rank;
+        rc = render_shard_tiles_keyed(r, cam, p, deal.tiles.data() + deal.off[c->rank], deal.count(c->rank), key | 1u,
+                                      mine, st);
+    } else {
         rc = rt_render_shard(r, cam, p, (uint32_t)c->rank, (uint32_t)c->world, mine, st);
+    }
     if (rc != RT_OK) return rc;
     if (tv) HIP_TRY(hipEventRecord((*tv)[1], st));
-    if (!pipelined) {
-        if ((rc = gather(c, k, deal, st)) != RT_OK) return rc;   // in stream order after the render
+    if (!pipelined) {   // the gather on the communicator's stream after the render; the caller's
+                        // stream waits for it, then rank 0 assembles on it
+        HIP_TRY(hipEventRecord(c->ev_render[k], st));
+        HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_render[k], 0));
+        if ((rc = gather(c, k, deal, c->comm_stream)) != RT_OK) return rc;
+        HIP_TRY(hipEventRecord(c->ev_gather[k], c->comm_stream));
+        HIP_TRY(hipStreamWaitEvent(st, c->ev_gather[k], 0));
         if (tv) HIP_TRY(hipEventRecord((*tv)[2], st));
-        if ((rc = assemble(c, r, k, rgb8_dev, st)) != RT_OK) return rc;
+        if ((rc = assemble(c, k, rgb8_dev, st)) != RT_OK) return rc;
         c->frames += 1;
         return RT_OK;
     }
-    // pipelined: this frame's gather runs on the communicator's stream while the caller's
-    // stream goes on (the next frame's render).  The previous frame is completed here: on rank
-    // 0 its unshuffle also runs on the communicator's stream, right behind its gather, so the
-    // render stream does not wait for it (only the render into its slot, one frame later, does)
+    // pipelined: this frame's gather runs beside the caller's stream's next work (the next
+    // frame's render).  The previous frame is completed here: on rank 0 its unshuffle runs on the
+    // communicator's stream right behind its gather, so the render stream does not wait for it
+    // (only the render into its slot, one frame later, does)
     if (c->pending >= 0) {
-        // frame i-1: assembled after its gather (stream order on the comm stream) and after the
-        // caller's earlier work on rgb8_dev; its buffers are rendered into again by the next
-        // call, which the render stream reaches only after this wait
         const int j = c->pending;
         if (c->rank == 0) {
             HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_caller, 0));
-            if ((rc = assemble(c, r, j, rgb8_dev, c->comm_stream)) != RT_OK) return rc;
+            if ((rc = assemble(c, j, rgb8_dev, c->comm_stream)) != RT_OK) return rc;
             HIP_TRY(hipEventRecord(c->ev_asm[j], c->comm_stream));
             HIP_TRY(hipStreamWaitEvent(st, c->ev_asm[j], 0));
         } else {
@@ -639,7 +720,7 @@ int rt_multi_flush(rt_renderer *r, rt_comm *c, uint32_t *rgb8_dev, void *stream)
     hipStream_t st = (hipStream_t)stream;
     const int j = c->pending;
     HIP_TRY(hipStreamWaitEvent(st, c->ev_gather[j], 0));
-    int rc = assemble(c, r, j, rgb8_dev, st);
+    int rc = assemble(c, j, rgb8_dev, st);
     if (rc != RT_OK) return rc;
     c->pending = -1;
     c->frames += 1;

@@ -229,6 +229,14 @@ class NativeShardedFrame:
         self._check(self.L.rt_comm_timing(self.h, C.byref(a), C.byref(b), C.byref(n)))
         return a.value, b.value, n.value
 
+    def deal_info(self):
+        """The deal frames are rendered under now (rt_comm_deal_info): {balanced, tiles, deals_built,
+        exchanges, moves, moves_skipped_on_reset}."""
+        b, t, st = C.c_int(), C.c_uint32(), (C.c_uint64 * 4)()
+        self._check(self.L.rt_comm_deal_info(self.h, C.byref(b), C.byref(t), None, st))
+        return {"balanced": b.value, "tiles": t.value, "deals_built": int(st[0]), "exchanges": int(st[1]),
+                "moves": int(st[2]), "moves_skipped_on_reset": int(st[3])}
+
     def close(self):
         h = getattr(self, "h", None)
         if h is not None and h.value:

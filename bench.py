@@ -345,8 +345,10 @@ def main():
             rms, gms, n = tm
             per = torch.tensor([rms / max(n, 1), gms / max(n, 1)], dtype=torch.float64, device=dev)
             dist.all_reduce(per, op=dist.ReduceOp.MAX)
+            di = sharded.deal_info()   # the deal this rank's frames actually ran under
             multi = {"exchange": "rt_render_frame_multi (RCCL send/recv to rank 0 from C++, pipelined)",
-                     "deal": "balanced (rt_tile_deal, RT_MULTI_BALANCED)" if args.scaling == "strong" else "interleaved t % N",
+                     "deal_requested": "balanced (RT_MULTI_BALANCED)" if args.scaling == "strong" else "interleaved t % N",
+                     "deal_rank0": {"in_use": "balanced" if di["balanced"] else "interleaved", **di},
                      "render_ms_per_frame_max_rank": round(per[0].item(), 4),
                      "gather_ms_per_frame_max_rank": round(per[1].item(), 4)}
         else:
@@ -361,6 +363,23 @@ def main():
     overlap = rend.overlap()
     in_flight = rend.overlap_depth()
     choices = rend.choices() if args.depth == 1 else None   # the renderer's timed camera-walk / split choices
+    walk_check = None
+    if choices is not None and choices["walk"] == 1 and sharded is None:
+        # untimed: the wave camera walk's counters (lanes re-traced in the reference order, boxes
+        # entered through its cull margin) over 10 frames, then 10 frames re-tracing EVERY walked
+        # lane in the reference order and counting results that differ (rt_renderer_walk_stats)
+        rend.set_walk_check(rt.WALK_CHECK_COUNT)
+        for k in range(10):
+            step(nf + args.steps + 100 + k)
+        w1 = rend.walk_stats()
+        rend.set_walk_check(rt.WALK_CHECK_VERIFY)
+        for k in range(10):
+            step(nf + args.steps + 110 + k)
+        w2 = rend.walk_stats()
+        rend.set_walk_check(rt.WALK_CHECK_OFF)
+        walk_check = {"frames": 10, "rays_walked": w1["walked"], "lanes_retraced": w1["retraced"],
+                      "margin_boxes": w1["margin_boxes"], "verify_frames": 10,
+                      "verify_rays": w2["walked"] - w1["walked"], "verify_mismatch": w2["verify_mismatch"]}
     companion = None
     if world == 1 and args.depth == 1 and (W, H) == (1920, 1080) and not args.no_companion:   # the metric's other frame size
         # the measured renderer is done: free its streams first, so that the companion's
@@ -424,6 +443,8 @@ def main():
                                                     else "frames in flight serial, 2, 2, serial") + " (8 frames each)"}
             if choices is not None:   # walk 0 lane / 1 wave, split 0 plain / 1 half tiles; groups A, B, B, A
                 line["timed_choices"] = choices
+            if walk_check is not None:
+                line["camera_walk_check"] = walk_check
         if multi:
             line["multi_gpu"] = multi
         if companion:

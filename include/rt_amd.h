@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 enum {
     RT_OK = 0,
@@ -286,13 +286,15 @@ int rt_comm_destroy(rt_comm *c);
 #define RT_MULTI_PIPELINED 1u
 /* RT_MULTI_TIMING: HIP events around this rank's render and its gather, summed by rt_comm_timing */
 #define RT_MULTI_TIMING 2u
-/* RT_MULTI_BALANCED: from the 7th frame of a parameter set (camera, size, spp, depth, mode) on,
- * the ranks render the cost-balanced compact deal of rt_tile_deal instead of t % world: built
- * once per parameter set from every rank's measured tile costs (rt_renderer_tile_costs; where a
- * rank measured none -- path-traced frames -- the interleaved deal stays) in one exchange: the
- * costs to rank 0, the deal back to all.  When tiles change owner the ranks' accumulators are
- * merged first, so accumulation goes on exactly.  Frames are identical under any deal; every
- * rank must pass the same flags. */
+/* RT_MULTI_BALANCED: the ranks render the cost-balanced compact deal of rt_tile_deal instead of
+ * t % world once every rank has measured its tiles' costs (rt_renderer_tile_costs: wave cycles of
+ * primary+shadow tiles, level-0 cycles of path-traced ones).  A parameter set (camera, size, spp,
+ * depth, mode) tries on its 6th frame, then its 12th, 24th, ... until every rank has costs -- one
+ * all-gather of [status, costs] blocks, after which every rank builds the same deal -- and not
+ * again until a parameter changes; the deal in use is kept across camera moves.  When tiles
+ * change owner their accumulator values move to the new owner (point-to-point, in stream
+ * order), except on frames with reset set, so accumulation goes on exactly.  Frames are
+ * identical under any deal; every rank must pass the same flags. */
 #define RT_MULTI_BALANCED 4u
 int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, const rt_frame_params *p,
                           uint32_t *rgb8_dev, uint32_t flags, void *stream);
@@ -301,6 +303,11 @@ int rt_multi_flush(rt_renderer *r, rt_comm *c, uint32_t *rgb8_dev, void *stream)
  * this rank's shard render, gather_ms = from the render's end to the gather's completion
  * (exposed exchange latency; beside the next render in pipelined mode); resets the sums. */
 int rt_comm_timing(rt_comm *c, double *render_ms, double *gather_ms, uint64_t *frames);
+/* The deal frames are rendered under now (every argument but c may be NULL): *balanced = 1 for a
+ * cost-balanced deal, 0 for the interleaved one; *ntiles = this rank's tile count and tile_list
+ * (room for *ntiles) its global tile indices in render order; stats: [0] balanced deals built,
+ * [1] cost exchanges run, [2] accumulator moves run, [3] moves skipped on reset frames. */
+int rt_comm_deal_info(const rt_comm *c, int *balanced, uint32_t *ntiles, uint32_t *tile_list, uint64_t stats[4]);
 
 int rt_renderer_counters(rt_renderer *r, rt_counters *out);
 /* Overlapped primary+shadow frames (RT_PS_PIPELINE; no reference counterpart -- Renderer::Tick,
@@ -333,6 +340,25 @@ int rt_renderer_choices(const rt_renderer *r, int *walk, int *split, float walk_
  * frame of a parameter set on).  At most n entries are copied.  Diagnostics and cost-balanced
  * tile deals. */
 int rt_renderer_tile_costs(const rt_renderer *r, uint32_t *costs, uint32_t n, uint32_t *n_out);
+/* Checks of the wave-coherent camera walk (RT_WALK_WAVE, or RT_WALK_AUTO once timed faster) of a
+ * renderer's primary+shadow frames.  The walk always re-traces in the reference order every lane
+ * whose result could depend on the visiting order (an exact-distance tie, or a hit nearer than
+ * its leaf box's entry -- which covers every hit found in a box entered through the walk's 2^-18
+ * cull margin).  Beyond that:
+ *   RT_WALK_CHECK_OFF    (default) the production frame kernel, nothing counted;
+ *   RT_WALK_CHECK_COUNT  a build of the frame kernel that counts camera rays walked, lanes
+ *                        re-traced and boxes a lane entered only through the cull margin;
+ *   RT_WALK_CHECK_VERIFY that build also re-traces EVERY walked lane in the reference order
+ *                        (IntersectBVH, template/scene.h:285-320), keeps that result and counts the
+ *                        lanes whose walk result (id, t, u, v bits) differed -- a diagnostic.
+ * Frames are identical at every level. */
+enum { RT_WALK_CHECK_OFF = 0, RT_WALK_CHECK_COUNT = 1, RT_WALK_CHECK_VERIFY = 2 };
+int rt_renderer_set_walk_check(rt_renderer *r, int level);
+/* Cumulative camera-walk counters of the frames rendered at RT_WALK_CHECK_COUNT / _VERIFY
+ * (synchronises the device): out[0] camera rays the wave walk traced, out[1] boxes entered only
+ * through its cull margin, out[2] lanes re-traced in the reference order, out[3]
+ * RT_WALK_CHECK_VERIFY lanes whose walk result differed from the reference order's (0 expected). */
+int rt_renderer_walk_stats(rt_renderer *r, uint64_t out[4]);
 /* accumulator readback, W*H float4 */
 int rt_renderer_read_accumulator(rt_renderer *r, float *host_out);
 /* Name of the frame kernel rt_render_frame / rt_render_shard launch for these params

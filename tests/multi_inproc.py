@@ -5,14 +5,22 @@ through the in-process RCCL stand-in (tests/cpp/libinproc_rccl.so, selected by R
 real RCCL refuses two ranks on one device).  Run by tests/test_multi_inproc.py in a child
 process (the stand-in must be the process's first RCCL).
 
-Every rank renders its t % world tiles of the same frames; rank 0's assembled frames must equal
-a plain renderer's Tick frames bit for bit, every rank's accumulator must equal the plain
-accumulator on the pixels of its tiles, and the ranks' ray counts must add up to the plain
-renderer's.  In pipelined mode rank 0 copies each returned frame on its own stream WITHOUT a
-host sync before the next call (the next call's unshuffle must wait for that copy).
+Every rank renders its share of the same frames; rank 0's assembled frames must equal a plain
+renderer's Tick frames bit for bit (same cameras, same resets), every rank's accumulator must
+equal the plain accumulator on the pixels of its tiles (interleaved modes), and the ranks' ray
+counts must add up to the plain renderer's.  In pipelined mode rank 0 copies each returned frame
+on its own stream WITHOUT a host sync before the next call (the next call's unshuffle must wait
+for that copy).
 
-usage: multi_inproc.py WORLD {sync|pipelined|balanced} RECIPE WIDTH HEIGHT   -> exit 0 and a JSON line
-(balanced = pipelined + RT_MULTI_BALANCED: the cost-balanced deal from a parameter set's 7th frame)"""
+usage: multi_inproc.py WORLD MODE RECIPE WIDTH HEIGHT   -> exit 0 and a JSON line
+MODE: sync | pipelined -- the interleaved deal;
+      balanced -- pipelined + RT_MULTI_BALANCED: primary+shadow frames until the cost-balanced
+                  deal is on (each rank's renderer times its camera walk first), path-traced
+                  frames (level-0 costs: a second balanced deal), primary+shadow again;
+      moving   -- balanced, then the camera moves every frame with the accumulator reset (the
+                  deal is kept), then a new static camera (rebalanced; the switch frame resets);
+      ptbal    -- path-traced frames only (spp 16, depth 10), balanced on level-0 costs.
+The balanced modes print the communicator's deal_info and require the balanced deal at the end."""
 import ctypes as C
 import json
 import os
@@ -25,17 +33,51 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import advancedgraphicsraytracer_amd as rt  # noqa: E402
-from advancedgraphicsraytracer_amd.shard import shard_pixels  # noqa: E402
 
-# (spp, Trace depth) per frame: primary+shadow frames (past the tile-order tuning), a sample-
-# split frame, path-traced frames, primary+shadow again
-PLAN = [(1, 1)] * 6 + [(2, 1), (1, 3), (2, 4), (1, 1), (1, 1)]
-# balanced mode: the deal switches on the 7th frame of a parameter set (kDealAfter), so runs of
-# equal parameters: primary+shadow (measured costs), path-traced (equal costs), primary+shadow
-PLAN_BALANCED = [(1, 1)] * 10 + [(1, 3)] * 8 + [(2, 1)] * 3
+BALANCED_MODES = ("balanced", "moving", "ptbal")
 
 
-def rank_main(rank, world, uid, recipe, W, H, mode, results, errors):
+def plan_for(mode):
+    """[(spp, depth, camera shift, reset)] per frame"""
+    if mode in ("sync", "pipelined"):
+        # primary+shadow frames (past the tile-order tuning), a sample-split frame, path-traced
+        # frames, primary+shadow again
+        return [(s, d, 0, False) for s, d in [(1, 1)] * 6 + [(2, 1), (1, 3), (2, 4), (1, 1), (1, 1)]]
+    if mode == "balanced":
+        # the walk is timed over frames 1-16 and the costs exist from frame 17: the attempts on
+        # frames 6 and 12 find none, the one on frame 24 builds the deal (INPROC_PS_FRAMES: more
+        # primary+shadow frames, for runs with a tuning delay)
+        n = int(os.environ.get("INPROC_PS_FRAMES", "30"))
+        return [(1, 1, 0, False)] * n + [(1, 3, 0, False)] * 10 + [(2, 1, 0, False)] * 3
+    if mode == "moving":
+        static = [(1, 1, 0, False)] * 30
+        moving = [(1, 1, k, True) for k in range(1, 11)]             # every frame a new camera, reset
+        settle = [(1, 1, 11, f == 0 or f == 6) for f in range(20)]   # new static camera; its 6th frame
+        return static + moving + settle                              # (the rebalancing one) resets
+    if mode == "ptbal":
+        return [(16, 10, 0, False)] * 10
+    raise SystemExit(f"unknown mode {mode}")
+
+
+def tile_pixels(W, H, tiles):
+    """pixel indices of the listed 8x8 tiles (on screen only)"""
+    tx = (W + 7) // 8
+    lane = np.arange(64)
+    t = np.asarray(tiles, np.int64)[:, None]
+    x, y = (t % tx) * 8 + lane % 8, (t // tx) * 8 + lane // 8
+    return (y * W + x)[(x < W) & (y < H)]
+
+
+def camera_for(W, H, shift):
+    cam = rt.Camera.default(W, H)
+    if shift:   # a sideways move, as Camera::AdjustCamera does for the arrow keys (camera.h:54-86)
+        d = 0.01 * shift
+        for f in ("pos", "top_left", "top_right", "bottom_left"):
+            getattr(cam, f)[0] += d
+    return cam
+
+
+def rank_main(rank, world, uid, recipe, W, H, mode, plan, results, errors):
     try:
         L = rt.lib()
         torch.cuda.set_device(0)
@@ -47,22 +89,33 @@ def rank_main(rank, world, uid, recipe, W, H, mode, results, errors):
         out = torch.zeros(W * H, dtype=torch.int32, device="cuda:0") if rank == 0 else None
         optr = C.c_void_p(out.data_ptr()) if rank == 0 else None
         pipelined = mode != "sync"
-        flags = (rt.MULTI_PIPELINED if pipelined else 0) | (rt.MULTI_BALANCED if mode == "balanced" else 0)
-        plan = PLAN_BALANCED if mode == "balanced" else PLAN
-        copies = []
+        flags = (rt.MULTI_PIPELINED if pipelined else 0) | (rt.MULTI_BALANCED if mode in BALANCED_MODES else 0)
+        copies, deals = [], []
         with torch.cuda.stream(st):
-            for f, (spp, depth) in enumerate(plan):
-                p = r.params(spp, depth, f)
-                rt._check(L.rt_render_frame_multi(r.h, h, C.byref(r.camera), C.byref(p), optr, flags,
+            for f, (spp, depth, shift, reset) in enumerate(plan):
+                cam = camera_for(W, H, shift)
+                p = r.params(spp, depth, f, reset)
+                rt._check(L.rt_render_frame_multi(r.h, h, C.byref(cam), C.byref(p), optr, flags,
                                                   C.c_void_p(st.cuda_stream)))
                 if rank == 0 and (not pipelined or f > 0):
                     copies.append(out.clone())       # on st: no host sync before the next call
+                b = C.c_int()
+                rt._check(L.rt_comm_deal_info(h, C.byref(b), None, None, None))
+                deals.append(b.value)
             if pipelined:
                 rt._check(L.rt_multi_flush(r.h, h, optr, C.c_void_p(st.cuda_stream)))
                 if rank == 0:
                     copies.append(out.clone())
         st.synchronize()
-        results[rank] = {"frames": [c.cpu().numpy() for c in copies], "acc": r.accumulator(), "counters": r.counters()}
+        b, t, stats = C.c_int(), C.c_uint32(), (C.c_uint64 * 4)()
+        rt._check(L.rt_comm_deal_info(h, C.byref(b), C.byref(t), None, stats))
+        mine = np.zeros(t.value, np.uint32)
+        rt._check(L.rt_comm_deal_info(h, None, C.byref(t), mine.ctypes.data_as(C.POINTER(C.c_uint32)), None))
+        results[rank] = {"frames": [c.cpu().numpy() for c in copies], "acc": r.accumulator(), "counters": r.counters(),
+                         "tiles": mine,
+                         "deal": {"balanced": b.value, "tiles": t.value, "deals_built": int(stats[0]),
+                                  "exchanges": int(stats[1]), "moves": int(stats[2]), "moves_skipped": int(stats[3])},
+                         "deal_per_frame": deals}
         rt._check(L.rt_comm_destroy(h))
         r.close()
         scene.close()
@@ -72,37 +125,51 @@ def rank_main(rank, world, uid, recipe, W, H, mode, results, errors):
 
 def main():
     world, mode, recipe, W, H = int(sys.argv[1]), sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+    plan = plan_for(mode)
     L = rt.lib()
     uid = (C.c_uint8 * rt.RT_COMM_ID_BYTES)()
     rt._check(L.rt_comm_unique_id(uid))
     results, errors = [None] * world, []
-    threads = [threading.Thread(target=rank_main, args=(k, world, uid, recipe, W, H, mode, results, errors))
+    threads = [threading.Thread(target=rank_main, args=(k, world, uid, recipe, W, H, mode, plan, results, errors))
                for k in range(world)]
     for t in threads:
         t.start()
     for t in threads:
-        t.join(timeout=240)
+        t.join(timeout=400)
     if errors or any(t.is_alive() for t in threads):
         print(json.dumps({"ok": False, "errors": errors, "alive": [t.is_alive() for t in threads]}), flush=True)
         sys.exit(1)
-    plan = PLAN_BALANCED if mode == "balanced" else PLAN
     ref = rt.Renderer(rt.Scene.recipe(recipe), W, H)
-    want = [ref.tick_host(spp=spp, depth=depth, frame=f).view(np.int32) for f, (spp, depth) in enumerate(plan)]
+    want = []
+    for f, (spp, depth, shift, reset) in enumerate(plan):
+        ref.camera = camera_for(W, H, shift)
+        want.append(ref.tick_host(spp=spp, depth=depth, frame=f, reset=reset).view(np.int32))
     got = results[0]["frames"]
-    bad_frames = [f for f in range(len(plan)) if not np.array_equal(got[f], want[f])]
+    bad_frames = [f for f in range(len(plan)) if f >= len(got) or not np.array_equal(got[f], want[f])]
     acc = ref.accumulator()
     bad_acc = []
-    if mode != "balanced":   # (under a deal switch a pixel's accumulator lives on two ranks)
-        for k in range(world):
-            px = shard_pixels(W, H, k, world)
-            px = px[px >= 0]
-            if not np.array_equal(results[k]["acc"][px].view(np.uint32), acc[px].view(np.uint32)):
-                bad_acc.append(k)
+    for k in range(world):   # each rank holds the running averages of the tiles of its final deal
+        px = tile_pixels(W, H, results[k]["tiles"])
+        if not np.array_equal(results[k]["acc"][px].view(np.uint32), acc[px].view(np.uint32)):
+            bad_acc.append(k)
     c = ref.counters()
     sums = {key: sum(results[k]["counters"][key] for k in range(world)) for key in ("primary", "shadow", "bounce")}
-    ok = len(got) == len(plan) and not bad_frames and not bad_acc and all(sums[key] == c[key] for key in sums)
+    deal = results[0]["deal"]
+    deal_ok = True
+    if mode in BALANCED_MODES and world > 1:
+        # every rank ends on the same balanced deal, having built at least one
+        deal_ok = all(results[k]["deal"]["balanced"] == 1 and results[k]["deal"]["deals_built"] >= 1 for k in range(world))
+        if mode == "balanced":   # the primary+shadow deal, then a second one from path-traced costs
+            deal_ok = deal_ok and deal["deals_built"] >= 2 and deal["moves"] >= 2
+        if mode == "moving":     # no deal change while the camera moves; a rebalance afterwards
+            per = results[0]["deal_per_frame"]
+            deal_ok = deal_ok and per[30:40] == [per[29]] * 10 and deal["deals_built"] >= 2
+    ok = len(got) == len(plan) and not bad_frames and not bad_acc and all(sums[key] == c[key] for key in sums) and deal_ok
     print(json.dumps({"ok": ok, "world": world, "mode": mode, "frames": len(got), "bad_frames": bad_frames,
-                      "bad_acc_ranks": bad_acc, "counters": sums, "want_counters": {k: c[k] for k in sums}}), flush=True)
+                      "bad_acc_ranks": bad_acc, "counters": sums, "want_counters": {k: c[k] for k in sums},
+                      "deal": deal, "deal_ok": deal_ok,
+                      "first_balanced_frame": next((f for f, b in enumerate(results[0]["deal_per_frame"]) if b), None)}),
+          flush=True)
     sys.exit(0 if ok else 1)
 
 

@@ -115,6 +115,16 @@ def frame_vs_oracle(rt, g, o, W, H, spp, depth, frames=1, exact=True, whitted=Fa
     return got, want, gacc, acc, c, total
 
 
+def assert_acc_bits(gacc, acc):
+    """Accumulators bit for bit (every float4 component, weights included); on a mismatch the
+    message names the first differing pixel and the largest difference."""
+    g, w = gacc.view(np.uint32), acc.view(np.uint32)
+    if not np.array_equal(g, w):
+        bad = np.nonzero((g != w).any(axis=1))[0]
+        raise AssertionError(f"{len(bad)} accumulator pixels differ in their bits; first {bad[:3].tolist()}: "
+                             f"{gacc[bad[0]].tolist()} vs {acc[bad[0]].tolist()}, max |d| {np.abs(gacc - acc).max()}")
+
+
 def test_primary_plus_shadow_frame_1080p_bit_exact(rt, scenes):
     """Config 2 workload (teapot 1080p, 1 spp, primary + shadow = Trace depth 1)."""
     g, o = scenes("teapotF")
@@ -348,8 +358,7 @@ def test_packet_random_rays_and_partial_packet(scenes):
 
 def packet_check(rt, g, o, W, H, spp, depth, frames=1):
     got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, W, H, spp, depth, frames=frames, mode=rt.MODE_PACKET)
-    d = np.abs(gacc - acc)
-    assert d.max() <= PIX_TOL, d.max()
+    assert_acc_bits(gacc, acc)
     assert np.array_equal(got, want), f"{(got != want).sum()} RGB8 mismatches"
     assert c["shadow"] == st["shadow"]
     assert c["bounce"] == st["isect"] - W * H * spp * frames
@@ -474,8 +483,6 @@ def test_frame_kernel_name(rt):
     ("cfg3", 64, 48, 2, 32, {}),                                # the deepest Trace (32): meta bits, records
     ("cfg3", 136, 80, 4, 4, {"RT_PT_LANES": "0"}),              # chunk kernel at every level
     ("teapotF", 200, 120, 1, 10, {"RT_PT_LANES": "0", "RT_PT_DYNAMIC": "0"}),   # static chunks
-    ("cfg5", 160, 96, 4, 10, {"RT_PT_SORT": "3"}),              # levels 1-3 reordered (octant + cell)
-    ("cfg3", 136, 80, 4, 4, {"RT_PT_SORT": "9", "RT_PT_MEM_MB": "2"}),   # every level sorted, several batches
 ])
 def test_wavefront_equals_one_kernel_path_tracer(rt, torch, monkeypatch, recipe, W, H, spp, depth, env):
     """The wavefront path tracer (k_pt_level + k_pt_finish: compaction between bounce
@@ -617,7 +624,7 @@ def test_pipelined_frames_switch_to_serial_and_back(rt, torch, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("recipe,W,H,spp,depth,mode,shards", [
-    ("teapotF", 200, 120, 4, 1, 0, 1),      # primary+shadow, LDS kernel
+    ("teapotF", 200, 120, 4, 1, 0, 1),      # primary+shadow
     ("mig16", 160, 96, 3, 1, 0, 1),         # global-node kernel (wave walk AUTO)
     ("cfg3", 136, 80, 2, 6, 1, 1),          # Whitted
     ("teapotF", 200, 120, 8, 1, 0, 3),      # a 1/3 shard at spp 8 (the bench's N > 1 shape)
@@ -647,38 +654,6 @@ def test_sample_split_equals_whole_tiles(rt, torch, monkeypatch, recipe, W, H, s
         assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
     assert np.array_equal(ra.accumulator(), rb.accumulator())
     assert ra.counters() == rb.counters()
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["48", "64"])
-@pytest.mark.parametrize("spp,shards", [(1, 1), (4, 3)])
-def test_lds_node_kernels_equal_global_kernel(rt, torch, monkeypatch, kind, spp, shards):
-    """The opt-in LDS-node primary+shadow kernels (RT_LDS_KERNEL=48: 48-B pairs + u16
-    stacks, 2 x 512 threads; 64: 64-B pairs, 1024 threads) must give the global-node
-    kernel's frames bit for bit (whole frames and sample-split shards)."""
-    W, H = 200, 120
-    monkeypatch.setenv("RT_LDS_KERNEL", "0")
-    s_g = rt.Scene.recipe("teapotF")
-    monkeypatch.setenv("RT_LDS_KERNEL", kind)
-    s_l = rt.Scene.recipe("teapotF")
-    rg, rl = rt.Renderer(s_g, W, H), rt.Renderer(s_l, W, H)
-    assert rg.kernel_name(spp=spp, depth=1) == "k_render<path,1>"
-    assert rl.kernel_name(spp=spp, depth=1) == ("k_render_lds48<1>" if kind == "48" else "k_render_lds<1>")
-    dev = torch.device("cuda", 0)
-    for f in range(2):
-        if shards == 1:
-            a, b = rg.tick_host(spp=spp, depth=1, frame=f), rl.tick_host(spp=spp, depth=1, frame=f)
-        else:
-            cap = rg.shard_capacity(shards)
-            ta = torch.zeros(cap, dtype=torch.int32, device=dev)
-            tb = torch.zeros(cap, dtype=torch.int32, device=dev)
-            rg.render_shard(ta, 2, shards, spp=spp, depth=1, frame=f)
-            rl.render_shard(tb, 2, shards, spp=spp, depth=1, frame=f)
-            torch.cuda.synchronize()
-            a, b = ta.cpu().numpy(), tb.cpu().numpy()
-        assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
-    assert np.array_equal(rg.accumulator(), rl.accumulator())
-    assert rg.counters() == rl.counters()
 
 
 @pytest.mark.gpu
@@ -728,9 +703,82 @@ def test_baseline_configs_full_size(rt, scenes, recipe, W, H, spp, depth, frames
     g, o = scenes(recipe)
     got, want, gacc, acc, c, st = frame_vs_oracle(rt, g, o, W, H, spp, depth, frames=frames)
     assert np.array_equal(got, want), f"{(got != want).sum()} RGB8 mismatches"
-    assert np.abs(gacc - acc).max() <= PIX_TOL
+    assert_acc_bits(gacc, acc)
     assert c["shadow"] == st["shadow"]
     assert c["bounce"] == st["isect"] - W * H * spp * frames
+
+
+# ---- the wave-coherent camera walk that config 4's timed choice picks, forced, at full size
+def tile_pixels(W, H, tiles):
+    """pixel index of every lane of the listed 8x8 tiles, [len(tiles), 64] (-1 off screen)"""
+    tx = (W + 7) // 8
+    lane = np.arange(64)
+    t = np.asarray(tiles, np.int64)[:, None]
+    x = (t % tx) * 8 + lane % 8
+    y = (t // tx) * 8 + lane // 8
+    return np.where((x < W) & (y < H), y * W + x, -1)
+
+
+@pytest.mark.parametrize("W,H,frames", [(1920, 1080, 5), (3840, 2160, 5)])
+def test_wave_walk_config4_full_size_bit_exact(rt, scenes, W, H, frames):
+    """Config 4 (mig29 x16, primary + shadow) with RT_WALK_WAVE forced on every frame -- the walk
+    the timed choice picks for it: RGB8, accumulator bits and the shadow-ray count of
+    every frame against the oracle's IntersectBVH order (template/scene.h:285-320).  Then two
+    frames with RT_WALK_CHECK_VERIFY: every walked lane is re-traced in the reference order and
+    compared -- no lane may differ -- and the walk's counters (rays walked, lanes re-traced, boxes
+    entered through the cull margin) are reported."""
+    g, o = rt.Scene.recipe("mig16"), scenes("mig16")[1]
+    g.set_camera_walk(rt.WALK_WAVE)
+    r = rt.Renderer(g, W, H)
+    acc = np.zeros((W * H, 4), np.float32)
+    shadow = 0
+    for f in range(frames + 2):
+        if f == frames:
+            r.set_walk_check(rt.WALK_CHECK_VERIFY)
+        got = r.tick_host(spp=1, depth=1, frame=f)
+        want, st = o.tick(W, H, acc, spp=1, depth=1, frame=f)
+        shadow += st["shadow"]
+        assert np.array_equal(got, want), f"frame {f}: {(got != want).sum()} RGB8 mismatches"
+    assert_acc_bits(r.accumulator(), acc)
+    assert r.counters()["shadow"] == shadow
+    ws = r.walk_stats()
+    print(f"wave walk {W}x{H}: {ws}")
+    assert ws["walked"] == 2 * W * H
+    assert ws["verify_mismatch"] == 0, ws
+    r.close()
+
+
+def test_wave_walk_config4_balanced_eighth_shard_bit_exact(rt, scenes):
+    """One rank's share of config 4 at N = 8 under the balanced deal (rt_tile_deal over a full
+    frame's measured tile costs; rt_render_shard_tiles) with the wave walk forced: the packed
+    tiles and the accumulator of every pixel in them equal the oracle's frame, 5 frames."""
+    W, H, frames = 1920, 1080, 5
+    g, o = rt.Scene.recipe("mig16"), scenes("mig16")[1]
+    g.set_camera_walk(rt.WALK_LANE)      # costs recorded on frame 1 (no walk timing first)
+    full = rt.Renderer(g, W, H)
+    for f in range(4):
+        full.tick_host(spp=1, depth=1, frame=f)
+    cost = full.tile_costs()
+    full.close()
+    assert cost.size == ((W + 7) // 8) * ((H + 7) // 8)
+    tiles, off = rt.tile_deal(W, H, 8, cost)
+    g.set_camera_walk(rt.WALK_WAVE)
+    import torch
+    for k in (0, 5):
+        mine = tiles[off[k]:off[k + 1]]
+        r = rt.Renderer(g, W, H)
+        buf = torch.zeros(len(mine) * 64, dtype=torch.int32, device="cuda:0")
+        acc = np.zeros((W * H, 4), np.float32)
+        px = tile_pixels(W, H, mine).reshape(-1)
+        on = px >= 0
+        for f in range(frames):
+            r.render_shard_tiles(buf, mine, spp=1, depth=1, frame=f)
+            torch.cuda.synchronize()
+            want, _ = o.tick(W, H, acc, spp=1, depth=1, frame=f)
+            got = buf.cpu().numpy().view(np.uint32)
+            assert np.array_equal(got[on], want[px[on]]), f"shard {k} frame {f}: {(got[on] != want[px[on]]).sum()} differ"
+        assert_acc_bits(r.accumulator()[px[on]], acc[px[on]])
+        r.close()
 
 
 # InitSeed maps exactly one base to 0, a fixed point of xorshift32 (every draw 0: the camera
@@ -747,37 +795,9 @@ def test_zero_seed_pixel_terminates_and_matches(rt, scenes, depth, spp):
     got = r.tick_host(spp=spp, depth=depth, frame=frame)
     acc = np.zeros((W * H, 4), np.float32)
     want, st = o.tick(W, H, acc, spp=spp, depth=depth, frame=frame)
-    assert np.abs(r.accumulator() - acc).max() <= PIX_TOL
+    assert_acc_bits(r.accumulator(), acc)
     assert np.array_equal(got, want)
     assert r.counters()["shadow"] == st["shadow"]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("recipe,spp,depth,tl", [("cfg5", 4, 10, "1"), ("cfg3", 2, 4, "1"), ("cfg5", 2, 6, "200"),
-                                                  ("teapotF", 2, 10, "1")])
-def test_treelet_lane_kernel_equals_default(rt, torch, monkeypatch, recipe, spp, depth, tl):
-    """RT_PT_TREELET: BFS-renumbered top pairs copied to LDS by a 1024-lane state machine.
-    At 1080p the bounce levels are large enough for the state machine (not the drain), so
-    this holds its frames, accumulators and ray counters to the default lane kernel's."""
-    W, H = 1920, 1080
-    monkeypatch.setenv("RT_PT_TREELET", "0")
-    s_a = rt.Scene.recipe(recipe)
-    monkeypatch.setenv("RT_PT_TREELET", tl)
-    s_b = rt.Scene.recipe(recipe)
-    ra, rb = rt.Renderer(s_a, W, H), rt.Renderer(s_b, W, H)
-    for f in range(2):
-        a = ra.tick_host(spp=spp, depth=depth, frame=f)
-        b = rb.tick_host(spp=spp, depth=depth, frame=f)
-        assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
-    assert np.array_equal(ra.accumulator(), rb.accumulator())
-    assert ra.counters() == rb.counters()
-    # the renumbered device tree answers the batched queries identically too
-    rays = random_rays(20000, 17)
-    ta, oa, ua, va = (x.cpu().numpy() for x in s_a.IntersectBVH(rays))
-    tb, ob, ub, vb = (x.cpu().numpy() for x in s_b.IntersectBVH(rays))
-    assert np.array_equal(oa, ob) and np.array_equal(ta.view(np.uint32), tb.view(np.uint32))
-    assert np.array_equal(s_a.IsOccluded(rays).cpu().numpy(), s_b.IsOccluded(rays).cpu().numpy())
-    assert np.array_equal(s_a.bvh()[0], s_b.bvh()[0])     # rt_scene_copy_bvh keeps the reference order
 
 
 def assert_ties(rt, oracle, recipe, rays, t, obj, wobj):

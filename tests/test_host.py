@@ -90,7 +90,7 @@ def test_default_recipe_from_reference_assets(rt, oracle, reference_assets):
 
 
 def test_abi_version_and_device_count(rt):
-    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 3
+    assert rt.lib().rt_abi_version() == rt.ABI_VERSION == 4
     assert rt.device_count() >= 0
 
 

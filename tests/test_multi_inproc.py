@@ -1,4 +1,4 @@
-"""rt_render_frame_multi with world 2 and 3 on the box's one GPU: the ranks run as threads of a
+"""rt_render_frame_multi with world 1, 2, 3 and 8 on the box's one GPU: the ranks run as threads of a
 child process (tests/multi_inproc.py) whose exchange is the in-process RCCL stand-in
 (tests/cpp/libinproc_rccl.so via RT_RCCL_LIB).  Exercises every rank != 0 branch of
 csrc/rt_multi.cpp -- the send, rank 0's receive loop over its peers, the double-buffered tile and
@@ -29,16 +29,40 @@ def test_standin_library_exports_the_rccl_subset():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,mode,recipe,W,H", [(2, "sync", "teapotF", 200, 120), (2, "pipelined", "teapotF", 200, 120),
-                                                   (3, "sync", "cfg3", 136, 80), (3, "pipelined", "mig16", 200, 120),
-                                                   (3, "pipelined", "teapotF", 16, 8), (2, "balanced", "teapotF", 200, 120),
-                                                   (3, "balanced", "mig16", 256, 144), (1, "balanced", "cfg3", 136, 80)])
+@pytest.mark.parametrize("world,mode,recipe,W,H", [
+    (2, "sync", "teapotF", 200, 120), (2, "pipelined", "teapotF", 200, 120),
+    (3, "sync", "cfg3", 136, 80), (3, "pipelined", "mig16", 200, 120),
+    (3, "pipelined", "teapotF", 16, 8),                # ragged: a rank without a tile
+    (2, "balanced", "teapotF", 200, 120), (3, "balanced", "mig16", 256, 144), (1, "balanced", "cfg3", 136, 80),
+    (3, "moving", "teapotF", 200, 120),                # camera moves every frame: the deal is kept
+    (8, "pipelined", "teapotF", 1920, 1080),           # the driver's default N = 8 run (weak config 2 deal)
+    (8, "balanced", "mig16", 1920, 1080),              # config 4 at N = 8: balanced + pipelined, two switches
+    (8, "ptbal", "cfg5", 480, 270),                    # config 5's scene at N = 8: path-traced balanced deal
+])
 def test_multi_frame_world_n_on_one_gpu(world, mode, recipe, W, H):
     assert os.path.exists(STANDIN), "tests/cpp/libinproc_rccl.so must be built beforehand (__graft_entry__.build())"
     env = dict(os.environ, RT_RCCL_LIB=STANDIN)
     p = subprocess.run([sys.executable, "-u", DRIVER, str(world), mode, recipe, str(W), str(H)], env=env,
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=500)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert p.returncode == 0 and lines, f"rc {p.returncode}\n{p.stdout[-2000:]}\n{p.stderr[-2000:]}"
     res = json.loads(lines[-1])
+    print(json.dumps(res))
+    assert res["ok"], res
+
+
+@pytest.mark.gpu
+def test_balanced_deal_with_default_tune_delay():
+    """The bench's setting (RT_TUNE_DELAY_MS unset = 100 ms of GPU time before a renderer times its
+    camera walk, so its tile costs come late): the cost exchange is retried (frames 6, 12, 24, ...)
+    until every rank has costs and the balanced deal then takes over -- here with a short delay so
+    the run stays small (mig16, whose walk is timed)."""
+    assert os.path.exists(STANDIN)
+    env = dict(os.environ, RT_RCCL_LIB=STANDIN, RT_TUNE_DELAY_MS="3", INPROC_PS_FRAMES="400")
+    p = subprocess.run([sys.executable, "-u", DRIVER, "2", "balanced", "mig16", "256", "144"], env=env,
+                       capture_output=True, text=True, timeout=500)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and lines, f"rc {p.returncode}\n{p.stdout[-2000:]}\n{p.stderr[-2000:]}"
+    res = json.loads(lines[-1])
+    print(json.dumps(res))
     assert res["ok"], res

@@ -25,12 +25,13 @@ for s in "$@"; do
             step shard_mig 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --deal interleaved,balanced --out gpurun_out/shard_time.jsonl
             step shard_tp 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene teapotF --deal interleaved,balanced --out gpurun_out/shard_time.jsonl ;;
         shard5)
-            step shard_cfg5 600 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --deal interleaved,balanced --ranks last --out gpurun_out/shard_time.jsonl
-            step shard_cfg3 600 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg3 --depth 4 --spp 4 --warm 6 --frames 6 --deal interleaved,balanced --ranks last --out gpurun_out/shard_time.jsonl ;;
+            step shard_cfg5 900 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --deal interleaved,balanced --ranks all --out gpurun_out/shard_time.jsonl
+            step shard_cfg3 900 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg3 --depth 4 --spp 4 --warm 6 --frames 6 --deal interleaved,balanced --ranks all --out gpurun_out/shard_time.jsonl ;;
         region) step region 300 python tools/timed_region.py --out gpurun_out/timed_region.jsonl ;;
-        sortab)
-            step sortab_c5 600 env GPU_MAX_HW_QUEUES=8 python tools/knob_ab.py --scene cfg5 --spp 16 --depth 10 --var RT_PT_SORT=0 --var RT_PT_SORT=1 --var RT_PT_SORT=3 --check --out gpurun_out/knob_ab.jsonl
-            step sortab_c3 600 env GPU_MAX_HW_QUEUES=8 python tools/knob_ab.py --scene cfg3 --spp 4 --depth 4 --var RT_PT_SORT=0 --var RT_PT_SORT=1 --var RT_PT_SORT=3 --check --out gpurun_out/knob_ab.jsonl ;;
+        parity4)   # round 4: the forced wave walk at full size, bit-exact accumulators, the deal machinery
+            step parity4 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "wave_walk_config4 or baseline_configs or zero_seed or packet or primary_plus_shadow" -s ;;
+        multi4)
+            step multi4 1100 python -u -m pytest tests/test_multi_inproc.py -m gpu -q -p no:cacheprovider --timeout 520 --timeout-method thread -s ;;
         benchcfg)
             step bench_cfg3 300 python bench.py --config 3 --steps 30 --warmup 3 --no-cpu-baseline
             step bench_cfg4 300 python bench.py --config 4 --steps 30 --warmup 5 --no-cpu-baseline

@@ -159,8 +159,9 @@ def main():
     if mode in BALANCED_MODES and world > 1:
         # every rank ends on the same balanced deal, having built at least one
         deal_ok = all(results[k]["deal"]["balanced"] == 1 and results[k]["deal"]["deals_built"] >= 1 for k in range(world))
-        if mode == "balanced":   # the primary+shadow deal, then a second one from path-traced costs
-            deal_ok = deal_ok and deal["deals_built"] >= 2 and deal["moves"] >= 2
+        if mode == "balanced":   # the primary+shadow deal, then a rebalance on path-traced costs (which
+            # may cut the frame where the first deal did); every new deal moved the accumulators
+            deal_ok = deal_ok and deal["exchanges"] >= 2 and deal["moves"] == deal["deals_built"]
         if mode == "moving":     # no deal change while the camera moves; a rebalance afterwards
             per = results[0]["deal_per_frame"]
             deal_ok = deal_ok and per[30:40] == [per[29]] * 10 and deal["deals_built"] >= 2

@@ -27,6 +27,9 @@ for s in "$@"; do
         shard5)
             step shard_cfg5 900 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --deal interleaved,balanced --ranks all --out gpurun_out/shard_time.jsonl
             step shard_cfg3 900 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg3 --depth 4 --spp 4 --warm 6 --frames 6 --deal interleaved,balanced --ranks all --out gpurun_out/shard_time.jsonl ;;
+        overhead)  # world-1 cost of the multi-GPU frame path against Tick (host submission, assembly)
+            step oh_tp 300 env GPU_MAX_HW_QUEUES=8 python tools/multi_overhead.py --scene teapotF --frames 400 --events none
+            step oh_mig 300 env GPU_MAX_HW_QUEUES=8 python tools/multi_overhead.py --scene mig16 --frames 400 --events none ;;
         region) step region 300 python tools/timed_region.py --out gpurun_out/timed_region.jsonl ;;
         parity4)   # round 4: the forced wave walk at full size, bit-exact accumulators, the deal machinery
             step parity4 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "wave_walk_config4 or baseline_configs or zero_seed or packet or primary_plus_shadow" -s ;;

@@ -46,8 +46,13 @@ def main():
     ap.add_argument("--top", type=int, default=20)
     a = ap.parse_args()
     lines = parse(a.asm, a.symbol)
+    files = {}
+    for ln in open(a.asm):   # the .file table precedes the kernels
+        p = ln.split()
+        if len(p) >= 4 and p[0] == ".file" and p[1].isdigit():
+            files[p[1]] = p[3].strip('"')
     # instructions with their block structure and source line
-    insts, blocks, cur_loc, files = [], [], None, {}
+    insts, blocks, cur_loc = [], [], None
     labels = {}
     for ln in lines:
         s = ln.strip()
@@ -134,18 +139,27 @@ def main():
         if c >= peak - 1 and shown < a.top:
             shown += 1
             print(f"  {c:4d}  {insts[i][5][:90]}  ({where(insts[i][4])})")
-    # the live set at the first peak: each register with the source line of its nearest earlier
-    # definition in program order (an approximation of the reaching definition)
+    # the live set at the first peak: each register with the source lines of its reaching
+    # definitions (backwards through the control flow graph)
+    pred = collections.defaultdict(list)
+    for i, js in succ.items():
+        for j in js:
+            pred[j].append(i)
     i0 = counts.index(peak)
     print(f"live at the first peak (instruction {i0}, {where(insts[i0][4])}):")
     groups = collections.defaultdict(list)
     for r in sorted(live_in[i0]):
-        loc = None
-        for j in range(i0 - 1, -1, -1):
+        locs, seen, todo = set(), {i0}, list(pred[i0])
+        while todo and len(locs) < 4:
+            j = todo.pop()
+            if j in seen:
+                continue
+            seen.add(j)
             if r in insts[j][2]:
-                loc = insts[j][4]
-                break
-        groups[where(loc)].append(r)
+                locs.add(where(insts[j][4]))
+                continue
+            todo.extend(pred[j])
+        groups[" / ".join(sorted(locs)) or "?"].append(r)
     for w, rs in sorted(groups.items(), key=lambda kv: -len(kv[1])):
         print(f"  {len(rs):3d}  defined at {w}: v{rs}")
 

@@ -65,7 +65,9 @@ struct FrameArgs {
     float4 *samples;                    // non-null: per-sample values [spp][ntiles_local][64] (sample
                                         // split, overlapped frames); k_pt_finish accumulates them
     int packed_out;
-    const uint32_t *order;              // tile dispatch order: local tile of slot i (nullptr = identity)
+    const uint32_t *order;              // tile dispatch order: local tile of slot i (nullptr = identity); an
+                                        // entry with bit 31 renders part (bits 28-30) of its tile only
+    uint32_t part_shift;                // lanes per part of a split tile = 1 << part_shift (5: halves)
     uint32_t *tile_cost;                // if set: each tile's wave cycles (to build the order)
     float4 *acc;
     uint32_t *out;
@@ -117,6 +119,11 @@ struct PathArgs {
     float4 *sum;
     uint32_t *tile_cost;                 // level 0: if set, each local tile's wave cycles (summed over its
                                          // samples) are added here -- a multi-GPU deal's cost map
+    // split bounce levels (RT_PT_SPLIT): per path a hit record (t, obj, u, v; then the shadow ray's
+    // occluded flag) and the NEE record (I, tmax | L, q | BRDF, rc); the shadow queue (segments of
+    // seg_cap entries) with its counts and head counters, laid out as qcount / qhead
+    float4 *hit, *aux;
+    uint32_t *squeue, *scount, *shead;
 };
 
 // Batched Renderer::Trace / WhittedTrace on caller rays (rt_trace): one lane per ray.
@@ -145,6 +152,8 @@ struct TraceArgs {
     int launch_pt_level(const SceneView &S, const FrameArgs &F, const PathArgs &P, bool tex,      \
                         size_t lds, uint32_t num_cus, hipStream_t st);                            \
     void launch_pt_lanes(const SceneView &S, const FrameArgs &F, const PathArgs &P, bool tex,     \
+                         size_t lds, uint32_t num_cus, hipStream_t st);                           \
+    void launch_pt_split(const SceneView &S, const FrameArgs &F, const PathArgs &P, bool tex,     \
                          size_t lds, uint32_t num_cus, hipStream_t st);                           \
     void launch_pt_finish(const FrameArgs &F, const PathArgs &P, bool last, hipStream_t st);      \
     void launch_trace(const SceneView &S, const TraceArgs &A, int mode, int md, bool tex,         \

@@ -58,6 +58,7 @@ struct rt_scene {
     int walk = RT_WALK_LANE;    // camera-ray walk of the global-node primary+shadow kernel
     bool ext = false;           // needs the kext kernels (cubes, quads, textures, non-Light light)
     bool pt_lanes = true;           // levels >= 1 run the lane state machine (RT_PT_LANES=0: k_pt_level)
+    bool pt_split = false;          // levels >= 1 run split traversal / shading launches (RT_PT_SPLIT=1)
     bool pt_dynamic = true;         // wavefront levels >= 1 fetch chunks dynamically (RT_PT_DYNAMIC=0: static)
     bool pt_wavefront = true;   // depth >= 2 path tracing: wavefront (k_pt_level) vs one kernel (k_render)
     uint32_t pt_drain_level = 64;   // bounce level from which the wavefront always drains (64 = never forced)
@@ -66,6 +67,7 @@ struct rt_scene {
     uint32_t split_units = 40000;   // sample split below this many tiles (1080p = 32,400 tiles)
     bool xcd_order = false;         // measured order grouped by XCD: blocks b, b + 8, ... (one XCD) render
                                     // one compact screen region of 1/8 of the frame's cost (L2 locality)
+    uint32_t split_parts = 2;       // ... each as this many waves of 64 / parts lanes (RT_SPLIT_PARTS: 2, 4, 8)
     int32_t heavy_split = -1;       // primary+shadow frames: the costliest tiles run as two half-tile
                                     // waves (RT_SPLIT_HEAVY = count; -1: ntiles / 32)
     uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per slot (two when pipelined): 12 GB
@@ -111,7 +113,8 @@ struct rt_renderer {
     uint64_t order_key = 0;
     int order_state = 0;        // 0 idle, 1 costs recorded, 2 order active, 3 costs held without an
                                 // order (path-traced frames)
-    uint32_t order_split = 0;   // leading tiles of the split order that run as two half-tile units
+    uint32_t order_split = 0;   // leading tiles of the split order that run as order_parts units each
+    uint32_t order_parts = 2;
     int split_phase = -1;       // -1 decided / not tried; 0 .. 4 kTuneGroup - 1 timing frames in groups
                                 // (plain, split, split, plain), 4 kTuneGroup decide
     bool use_split = false;     // the split order measured faster
@@ -579,6 +582,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_PT_WAVEFRONT")) s->pt_wavefront = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_DYNAMIC")) s->pt_dynamic = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_LANES")) s->pt_lanes = std::atoi(e) != 0;
+    if (const char *e = std::getenv("RT_PT_SPLIT")) s->pt_split = std::atoi(e) != 0;
     // RT_PT_DRAIN_LEVEL / RT_PT_MEM_MB: wavefront drain level and path-state budget (A/B runs)
     if (const char *e = std::getenv("RT_PT_DRAIN_LEVEL")) s->pt_drain_level = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_DRAIN_ROUNDS")) s->pt_drain_rounds = std::max(0.0, std::atof(e));
@@ -586,6 +590,10 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     // RT_SPLIT_UNITS: sample-split target units (0 = never split)
     if (const char *e = std::getenv("RT_SPLIT_UNITS")) s->split_units = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_SPLIT_HEAVY")) s->heavy_split = std::max(-1, std::atoi(e));
+    if (const char *e = std::getenv("RT_SPLIT_PARTS")) {
+        const int k = std::atoi(e);
+        s->split_parts = k >= 8 ? 8u : k >= 4 ? 4u : 2u;
+    }
     // XCD-grouped tile order for scenes whose nodes + primitive slots exceed one XCD's 4 MB L2:
     // mig29 x16 (11.6 MB) 0.449 -> 0.406 ms; a cache-resident TEAPOT-F loses with it (4K
     // 0.377 -> 0.441 ms, 720p neutral) -- profiles/r02/ab_xcd_*.json.  RT_XCD_ORDER=0/1 forces it.
@@ -597,6 +605,9 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_PS_BUFFERS")) s->ps_buffers = (uint32_t)std::max(2, std::min(kPsMaxDepth + 1, std::atoi(e)));
     if (const char *e = std::getenv("RT_PS_DEPTH")) s->ps_depth = (uint32_t)std::max(2, std::min(kPsMaxDepth, std::atoi(e)));
     if (const char *e = std::getenv("RT_TUNE_DELAY_MS")) s->tune_delay_ms = (float)std::max(0.0, std::atof(e));
+    // split levels hold 72 B more per path (hit, NEE record, shadow queue): the same batches
+    // (all 16 spp of a 1080p depth-10 frame in one) need 16 GB per slot
+    if (s->pt_split) s->pt_mem_bytes = 16384ull << 20;
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
@@ -730,7 +741,8 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     // parity, up to 2 GB each); the serial path keeps them per batch with a running sum
     const uint64_t res_need = (uint64_t)F.spp * npix * 16u;
     const bool pipe = s->pt_pipeline && res_need <= (2ull << 30);
-    const uint64_t per_path = 32u + 16u + 8u + (uint64_t)(F.depth - 1) * 32u;
+    const bool split = s->pt_split;
+    const uint64_t per_path = 32u + 16u + 8u + (uint64_t)(F.depth - 1) * 32u + (split ? 16u + 48u + 8u : 0u);
     // per slot: two slots of up to RT_PT_MEM_MB each when pipelined (fewer, larger batches and
     // frame-to-frame overlap beat more batches: CFG5-sub 8.85 ms with half the budget per slot
     // -- two batches a frame -- vs 8.51 ms with one batch a frame, profiles/r02/bench_pipe_*)
@@ -741,10 +753,13 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     const uint64_t np = batch * npix;
     // queue segment k takes the survivors of chunks j = k (mod kQueueSegs); the grid's
     // wave count is a multiple of kQueueSegs, so a segment never gets more than this
-    const uint64_t seg_cap = ((np / 64u + kQueueSegs - 1) / kQueueSegs + 1) * 64u;
+    // (split levels: a queue takes the survivors of the shading and of the completion pass, each
+    // spread over the segments by chunk, so its segments hold up to twice as many)
+    const uint64_t seg_cap = ((np / 64u + kQueueSegs - 1) / kQueueSegs + 1) * 64u * (split ? 2u : 1u);
     const size_t qbytes = (size_t)seg_cap * kQueueSegs * 4u;
-    const size_t cbytes = (size_t)(F.depth + 1) * (2u * kQueueSegs) * 64u;   // queue counts + head counters
-    const size_t need = (size_t)(np * (per_path - 8u) + 2 * qbytes + cbytes + 4096u);
+    // queue counts + head counters (split: + the shadow queue's)
+    const size_t cbytes = (size_t)(F.depth + 1) * (2u * kQueueSegs) * 64u * (split ? 2u : 1u);
+    const size_t need = (size_t)(np * (per_path - (split ? 16u : 8u)) + (split ? 3 : 2) * qbytes + cbytes + 8192u);
     if (!r->d_sum) {   // one float4 per pixel of the whole frame (a shard uses its first npix)
         const size_t tiles = (size_t)((r->W + 7) / 8) * ((r->H + 7) / 8);
         HIP_TRY(hipMalloc(&r->d_sum, tiles * 64u * sizeof(float4)));
@@ -816,6 +831,13 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         P.qcount = reinterpret_cast<uint32_t *>(take(cbytes));
         P.seg_cap = (uint32_t)seg_cap;
         P.qhead = P.qcount + (size_t)(F.depth + 1) * kQueueSegs * 16u;
+        if (split) {
+            P.scount = P.qhead + (size_t)(F.depth + 1) * kQueueSegs * 16u;
+            P.shead = P.scount + (size_t)(F.depth + 1) * kQueueSegs * 16u;
+            P.squeue = reinterpret_cast<uint32_t *>(take(qbytes));
+            P.hit = reinterpret_cast<float4 *>(take(np * 16u));
+            P.aux = reinterpret_cast<float4 *>(take(np * 48u));
+        }
         P.dynamic = s->pt_dynamic ? 1 : 0;
         P.rec = reinterpret_cast<float4 *>(take((size_t)(F.depth - 1) * np * 32u));
         // per-path radiance, indexed (sample - s0) * npix + pixel
@@ -833,7 +855,10 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
             P.queue_in = (level & 1u) ? q1 : q0;
             P.queue_out = (level & 1u) ? q0 : q1;
             int resident = 0;
-            if (level > 0 && s->pt_lanes) {             // incoherent levels: the lane state machine
+            if (level > 0 && split) {                   // incoherent levels: traversal / shading launches
+                if (s->ext) kext::launch_pt_split(view, F, P, tex, lds, s->num_cus, X);
+                else kcore::launch_pt_split(view, F, P, tex, lds, s->num_cus, X);
+            } else if (level > 0 && s->pt_lanes) {      // incoherent levels: the lane state machine
                 if (s->ext) kext::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, X);
                 else kcore::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, X);
             } else {
@@ -888,9 +913,9 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
 // L2 then holds the nodes of its region only, not of the whole frame.  A group whose region
 // ran out takes tiles from the region with the most cost left.
 std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const uint32_t *map, const std::vector<uint32_t> &entries,
-                                        const std::vector<uint32_t> &cost) {
-    // entries: order entries (local tile | split bits); an entry's cost is its tile's, halved
-    // for a half-tile entry (bit 31)
+                                        const std::vector<uint32_t> &cost, uint32_t parts) {
+    // entries: order entries (local tile | split bits); an entry's cost is its tile's, divided
+    // by the parts of a split tile (bit 31)
     const uint32_t n = (uint32_t)entries.size();
     auto morton = [](uint32_t x, uint32_t y) {
         uint64_t m = 0;
@@ -902,10 +927,10 @@ std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const uint32_t *map,
     std::vector<double> ec(n);
     double total = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t e = entries[i], lt = e & 0x3fffffffu;
+        const uint32_t e = entries[i], lt = e & 0x0fffffffu;
         const uint32_t tile = map ? map[lt] : lt * F.nshards + F.shard;
-        code[i] = morton(tile % F.tiles_x, tile / F.tiles_x) * 4u + (e >> 30);
-        ec[i] = (e >> 31) ? 0.5 * cost[lt] : (double)cost[lt];
+        code[i] = morton(tile % F.tiles_x, tile / F.tiles_x) * 16u + (e >> 28);
+        ec[i] = (e >> 31) ? cost[lt] / (double)parts : (double)cost[lt];
         z[i] = i;
         total += ec[i];
     }
@@ -993,20 +1018,21 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
             const int32_t hs = r->scene->heavy_split;
             k = std::min<uint32_t>(n, hs < 0 ? n / 32u : (uint32_t)hs);
         }
+        // RT_SPLIT_PARTS: a split tile runs as 2 (rows 0-3 / 4-7), 4 or 8 waves of a part each
+        const uint32_t parts = r->scene->split_parts;
         std::vector<uint32_t> ent(ord), sp;
-        for (uint32_t i = 0; i < k; ++i) {
-            sp.push_back(ord[i] | 0x80000000u);
-            sp.push_back(ord[i] | 0xC0000000u);
-        }
+        for (uint32_t i = 0; i < k; ++i)
+            for (uint32_t q = 0; q < parts; ++q) sp.push_back(ord[i] | 0x80000000u | (q << 28));
         for (uint32_t i = k; i < n; ++i) sp.push_back(ord[i]);
         if (r->scene->xcd_order && split_ok) {   // both orders grouped by XCD (global-node frame kernel)
             const uint32_t *map = F.tile_map ? r->map_host.data() : nullptr;
-            ent = xcd_grouped_order(F, map, ord, cost);
-            sp = xcd_grouped_order(F, map, sp, cost);
+            ent = xcd_grouped_order(F, map, ord, cost, parts);
+            sp = xcd_grouped_order(F, map, sp, cost, parts);
         }
         ent.insert(ent.end(), sp.begin(), sp.end());
         HIP_TRY(hipMemcpy(r->d_order, ent.data(), ent.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         r->order_split = k;
+        r->order_parts = parts;
         r->order_state = 2;
         r->use_split = k > 0 && r->scene->heavy_split > 0;            // a forced count: no timing
         r->split_phase = (k > 0 && r->scene->heavy_split < 0) ? 0 : -1;
@@ -1028,7 +1054,8 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
             ++r->split_phase;
         }
         F.order = split ? r->d_order + n : r->d_order;
-        F.nunits = F.ntiles_local * F.nchunks + (split ? r->order_split : 0u);   // split only with nchunks 1
+        F.nunits = F.ntiles_local * F.nchunks + (split ? r->order_split * (r->order_parts - 1u) : 0u);   // split only with nchunks 1
+        F.part_shift = r->order_parts == 8 ? 3u : r->order_parts == 4 ? 4u : 5u;
     }
     return RT_OK;
 }

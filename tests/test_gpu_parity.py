@@ -483,6 +483,11 @@ def test_frame_kernel_name(rt):
     ("cfg3", 64, 48, 2, 32, {}),                                # the deepest Trace (32): meta bits, records
     ("cfg3", 136, 80, 4, 4, {"RT_PT_LANES": "0"}),              # chunk kernel at every level
     ("teapotF", 200, 120, 1, 10, {"RT_PT_LANES": "0", "RT_PT_DYNAMIC": "0"}),   # static chunks
+    ("teapotF", 200, 120, 1, 10, {"RT_PT_SPLIT": "1"}),         # split bounce levels
+    ("teapotF", 200, 120, 2, 10, {"RT_PT_SPLIT": "1", "RT_PT_DRAIN_ROUNDS": "0"}),   # split at every level
+    ("cfg5", 96, 64, 3, 10, {"RT_PT_SPLIT": "1", "RT_PT_MEM_MB": "2"}),            # split, uneven batches
+    ("cfg3", 64, 48, 2, 32, {"RT_PT_SPLIT": "1", "RT_PT_DRAIN_ROUNDS": "0"}),      # split, Trace depth 32
+    ("cfg3", 136, 80, 4, 4, {"RT_PT_SPLIT": "1"}),
 ])
 def test_wavefront_equals_one_kernel_path_tracer(rt, torch, monkeypatch, recipe, W, H, spp, depth, env):
     """The wavefront path tracer (k_pt_level + k_pt_finish: compaction between bounce
@@ -503,6 +508,27 @@ def test_wavefront_equals_one_kernel_path_tracer(rt, torch, monkeypatch, recipe,
         assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
     assert np.array_equal(r_wf.accumulator(), r_mk.accumulator())
     assert r_wf.counters() == r_mk.counters()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recipe,W,H,spp,depth", [("cfg5", 640, 360, 4, 10), ("cfg3", 640, 360, 4, 4),
+                                                  ("teapotF", 960, 540, 2, 10)])
+def test_split_levels_equal_lane_machine(rt, torch, monkeypatch, recipe, W, H, spp, depth):
+    """Split bounce levels (RT_PT_SPLIT=1: closest-hit traversal, shading, shadow traversal and
+    completion as four launches per level) against the lane state machine at larger sizes:
+    frames, accumulators and ray counters bit for bit over three frames."""
+    monkeypatch.setenv("RT_PT_WAVEFRONT", "1")
+    monkeypatch.setenv("RT_PT_SPLIT", "1")
+    s1 = rt.Scene.recipe(recipe)
+    monkeypatch.setenv("RT_PT_SPLIT", "0")
+    s0 = rt.Scene.recipe(recipe)
+    r1, r0 = rt.Renderer(s1, W, H), rt.Renderer(s0, W, H)
+    for f in range(3):
+        a = r1.tick_host(spp=spp, depth=depth, frame=f)
+        b = r0.tick_host(spp=spp, depth=depth, frame=f)
+        assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
+    assert_acc_bits(r1.accumulator(), r0.accumulator())
+    assert r1.counters() == r0.counters()
 
 
 @pytest.mark.gpu
@@ -685,6 +711,37 @@ def test_measured_tile_order_keeps_frames(rt, torch, monkeypatch, recipe, spp, m
             tb = torch.zeros(cap, dtype=torch.int32, device=dev)
             ra.render_shard(ta, 1, shards, spp=spp, depth=depth, frame=f)
             rb.render_shard(tb, 1, shards, spp=spp, depth=depth, frame=f)
+            torch.cuda.synchronize()
+            a, b = ta.cpu().numpy(), tb.cpu().numpy()
+        assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
+    assert np.array_equal(ra.accumulator(), rb.accumulator())
+    assert ra.counters() == rb.counters()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recipe,shards", [("mig16", 1), ("teapotF", 3)])
+@pytest.mark.parametrize("parts", ["4", "8"])
+def test_split_parts_keep_frames(rt, torch, monkeypatch, recipe, shards, parts):
+    """The costliest tiles split into 4 or 8 waves of 16 / 8 lanes (RT_SPLIT_PARTS, forced with
+    RT_SPLIT_HEAVY=64, XCD-grouped for mig16) give the frames of the unordered kernel: 12 frames."""
+    W, H = 200, 120
+    monkeypatch.setenv("RT_TILE_ORDER", "0")
+    s_a = rt.Scene.recipe(recipe)
+    monkeypatch.setenv("RT_TILE_ORDER", "1")
+    monkeypatch.setenv("RT_SPLIT_HEAVY", "64")
+    monkeypatch.setenv("RT_SPLIT_PARTS", parts)
+    s_b = rt.Scene.recipe(recipe)
+    ra, rb = rt.Renderer(s_a, W, H), rt.Renderer(s_b, W, H)
+    dev = torch.device("cuda", 0)
+    for f in range(12):
+        if shards == 1:
+            a, b = ra.tick_host(spp=1, depth=1, frame=f), rb.tick_host(spp=1, depth=1, frame=f)
+        else:
+            cap = ra.shard_capacity(shards)
+            ta = torch.zeros(cap, dtype=torch.int32, device=dev)
+            tb = torch.zeros(cap, dtype=torch.int32, device=dev)
+            ra.render_shard(ta, 1, shards, spp=1, depth=1, frame=f)
+            rb.render_shard(tb, 1, shards, spp=1, depth=1, frame=f)
             torch.cuda.synchronize()
             a, b = ta.cpu().numpy(), tb.cpu().numpy()
         assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"

@@ -119,11 +119,6 @@ struct PathArgs {
     float4 *sum;
     uint32_t *tile_cost;                 // level 0: if set, each local tile's wave cycles (summed over its
                                          // samples) are added here -- a multi-GPU deal's cost map
-    // split bounce levels (RT_PT_SPLIT): per path a hit record (t, obj, u, v; then the shadow ray's
-    // occluded flag) and the NEE record (I, tmax | L, q | BRDF, rc); the shadow queue (segments of
-    // seg_cap entries) with its counts and head counters, laid out as qcount / qhead
-    float4 *hit, *aux;
-    uint32_t *squeue, *scount, *shead;
 };
 
 // Batched Renderer::Trace / WhittedTrace on caller rays (rt_trace): one lane per ray.
@@ -152,8 +147,6 @@ struct TraceArgs {
     int launch_pt_level(const SceneView &S, const FrameArgs &F, const PathArgs &P, bool tex,      \
                         size_t lds, uint32_t num_cus, hipStream_t st);                            \
     void launch_pt_lanes(const SceneView &S, const FrameArgs &F, const PathArgs &P, bool tex,     \
-                         size_t lds, uint32_t num_cus, hipStream_t st);                           \
-    void launch_pt_split(const SceneView &S, const FrameArgs &F, const PathArgs &P, bool tex,     \
                          size_t lds, uint32_t num_cus, hipStream_t st);                           \
     void launch_pt_finish(const FrameArgs &F, const PathArgs &P, bool last, hipStream_t st);      \
     void launch_trace(const SceneView &S, const TraceArgs &A, int mode, int md, bool tex,         \

@@ -58,7 +58,6 @@ struct rt_scene {
     int walk = RT_WALK_LANE;    // camera-ray walk of the global-node primary+shadow kernel
     bool ext = false;           // needs the kext kernels (cubes, quads, textures, non-Light light)
     bool pt_lanes = true;           // levels >= 1 run the lane state machine (RT_PT_LANES=0: k_pt_level)
-    bool pt_split = false;          // levels >= 1 run split traversal / shading launches (RT_PT_SPLIT=1)
     bool pt_dynamic = true;         // wavefront levels >= 1 fetch chunks dynamically (RT_PT_DYNAMIC=0: static)
     bool pt_wavefront = true;   // depth >= 2 path tracing: wavefront (k_pt_level) vs one kernel (k_render)
     uint32_t pt_drain_level = 64;   // bounce level from which the wavefront always drains (64 = never forced)
@@ -582,7 +581,6 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_PT_WAVEFRONT")) s->pt_wavefront = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_DYNAMIC")) s->pt_dynamic = std::atoi(e) != 0;
     if (const char *e = std::getenv("RT_PT_LANES")) s->pt_lanes = std::atoi(e) != 0;
-    if (const char *e = std::getenv("RT_PT_SPLIT")) s->pt_split = std::atoi(e) != 0;
     // RT_PT_DRAIN_LEVEL / RT_PT_MEM_MB: wavefront drain level and path-state budget (A/B runs)
     if (const char *e = std::getenv("RT_PT_DRAIN_LEVEL")) s->pt_drain_level = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_DRAIN_ROUNDS")) s->pt_drain_rounds = std::max(0.0, std::atof(e));
@@ -605,9 +603,6 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_PS_BUFFERS")) s->ps_buffers = (uint32_t)std::max(2, std::min(kPsMaxDepth + 1, std::atoi(e)));
     if (const char *e = std::getenv("RT_PS_DEPTH")) s->ps_depth = (uint32_t)std::max(2, std::min(kPsMaxDepth, std::atoi(e)));
     if (const char *e = std::getenv("RT_TUNE_DELAY_MS")) s->tune_delay_ms = (float)std::max(0.0, std::atof(e));
-    // split levels hold 72 B more per path (hit, NEE record, shadow queue): the same batches
-    // (all 16 spp of a 1080p depth-10 frame in one) need 16 GB per slot
-    if (s->pt_split) s->pt_mem_bytes = 16384ull << 20;
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
@@ -741,8 +736,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     // parity, up to 2 GB each); the serial path keeps them per batch with a running sum
     const uint64_t res_need = (uint64_t)F.spp * npix * 16u;
     const bool pipe = s->pt_pipeline && res_need <= (2ull << 30);
-    const bool split = s->pt_split;
-    const uint64_t per_path = 32u + 16u + 8u + (uint64_t)(F.depth - 1) * 32u + (split ? 16u + 48u + 8u : 0u);
+    const uint64_t per_path = 32u + 16u + 8u + (uint64_t)(F.depth - 1) * 32u;
     // per slot: two slots of up to RT_PT_MEM_MB each when pipelined (fewer, larger batches and
     // frame-to-frame overlap beat more batches: CFG5-sub 8.85 ms with half the budget per slot
     // -- two batches a frame -- vs 8.51 ms with one batch a frame, profiles/r02/bench_pipe_*)
@@ -753,13 +747,10 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     const uint64_t np = batch * npix;
     // queue segment k takes the survivors of chunks j = k (mod kQueueSegs); the grid's
     // wave count is a multiple of kQueueSegs, so a segment never gets more than this
-    // (split levels: a queue takes the survivors of the shading and of the completion pass, each
-    // spread over the segments by chunk, so its segments hold up to twice as many)
-    const uint64_t seg_cap = ((np / 64u + kQueueSegs - 1) / kQueueSegs + 1) * 64u * (split ? 2u : 1u);
+    const uint64_t seg_cap = ((np / 64u + kQueueSegs - 1) / kQueueSegs + 1) * 64u;
     const size_t qbytes = (size_t)seg_cap * kQueueSegs * 4u;
-    // queue counts + head counters (split: + the shadow queue's)
-    const size_t cbytes = (size_t)(F.depth + 1) * (2u * kQueueSegs) * 64u * (split ? 2u : 1u);
-    const size_t need = (size_t)(np * (per_path - (split ? 16u : 8u)) + (split ? 3 : 2) * qbytes + cbytes + 8192u);
+    const size_t cbytes = (size_t)(F.depth + 1) * (2u * kQueueSegs) * 64u;   // queue counts + head counters
+    const size_t need = (size_t)(np * (per_path - 8u) + 2 * qbytes + cbytes + 4096u);
     if (!r->d_sum) {   // one float4 per pixel of the whole frame (a shard uses its first npix)
         const size_t tiles = (size_t)((r->W + 7) / 8) * ((r->H + 7) / 8);
         HIP_TRY(hipMalloc(&r->d_sum, tiles * 64u * sizeof(float4)));
@@ -831,13 +822,6 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         P.qcount = reinterpret_cast<uint32_t *>(take(cbytes));
         P.seg_cap = (uint32_t)seg_cap;
         P.qhead = P.qcount + (size_t)(F.depth + 1) * kQueueSegs * 16u;
-        if (split) {
-            P.scount = P.qhead + (size_t)(F.depth + 1) * kQueueSegs * 16u;
-            P.shead = P.scount + (size_t)(F.depth + 1) * kQueueSegs * 16u;
-            P.squeue = reinterpret_cast<uint32_t *>(take(qbytes));
-            P.hit = reinterpret_cast<float4 *>(take(np * 16u));
-            P.aux = reinterpret_cast<float4 *>(take(np * 48u));
-        }
         P.dynamic = s->pt_dynamic ? 1 : 0;
         P.rec = reinterpret_cast<float4 *>(take((size_t)(F.depth - 1) * np * 32u));
         // per-path radiance, indexed (sample - s0) * npix + pixel
@@ -855,10 +839,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
             P.queue_in = (level & 1u) ? q1 : q0;
             P.queue_out = (level & 1u) ? q0 : q1;
             int resident = 0;
-            if (level > 0 && split) {                   // incoherent levels: traversal / shading launches
-                if (s->ext) kext::launch_pt_split(view, F, P, tex, lds, s->num_cus, X);
-                else kcore::launch_pt_split(view, F, P, tex, lds, s->num_cus, X);
-            } else if (level > 0 && s->pt_lanes) {      // incoherent levels: the lane state machine
+            if (level > 0 && s->pt_lanes) {             // incoherent levels: the lane state machine
                 if (s->ext) kext::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, X);
                 else kcore::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, X);
             } else {

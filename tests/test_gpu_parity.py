@@ -483,11 +483,6 @@ def test_frame_kernel_name(rt):
     ("cfg3", 64, 48, 2, 32, {}),                                # the deepest Trace (32): meta bits, records
     ("cfg3", 136, 80, 4, 4, {"RT_PT_LANES": "0"}),              # chunk kernel at every level
     ("teapotF", 200, 120, 1, 10, {"RT_PT_LANES": "0", "RT_PT_DYNAMIC": "0"}),   # static chunks
-    ("teapotF", 200, 120, 1, 10, {"RT_PT_SPLIT": "1"}),         # split bounce levels
-    ("teapotF", 200, 120, 2, 10, {"RT_PT_SPLIT": "1", "RT_PT_DRAIN_ROUNDS": "0"}),   # split at every level
-    ("cfg5", 96, 64, 3, 10, {"RT_PT_SPLIT": "1", "RT_PT_MEM_MB": "2"}),            # split, uneven batches
-    ("cfg3", 64, 48, 2, 32, {"RT_PT_SPLIT": "1", "RT_PT_DRAIN_ROUNDS": "0"}),      # split, Trace depth 32
-    ("cfg3", 136, 80, 4, 4, {"RT_PT_SPLIT": "1"}),
 ])
 def test_wavefront_equals_one_kernel_path_tracer(rt, torch, monkeypatch, recipe, W, H, spp, depth, env):
     """The wavefront path tracer (k_pt_level + k_pt_finish: compaction between bounce
@@ -508,27 +503,6 @@ def test_wavefront_equals_one_kernel_path_tracer(rt, torch, monkeypatch, recipe,
         assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
     assert np.array_equal(r_wf.accumulator(), r_mk.accumulator())
     assert r_wf.counters() == r_mk.counters()
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("recipe,W,H,spp,depth", [("cfg5", 640, 360, 4, 10), ("cfg3", 640, 360, 4, 4),
-                                                  ("teapotF", 960, 540, 2, 10)])
-def test_split_levels_equal_lane_machine(rt, torch, monkeypatch, recipe, W, H, spp, depth):
-    """Split bounce levels (RT_PT_SPLIT=1: closest-hit traversal, shading, shadow traversal and
-    completion as four launches per level) against the lane state machine at larger sizes:
-    frames, accumulators and ray counters bit for bit over three frames."""
-    monkeypatch.setenv("RT_PT_WAVEFRONT", "1")
-    monkeypatch.setenv("RT_PT_SPLIT", "1")
-    s1 = rt.Scene.recipe(recipe)
-    monkeypatch.setenv("RT_PT_SPLIT", "0")
-    s0 = rt.Scene.recipe(recipe)
-    r1, r0 = rt.Renderer(s1, W, H), rt.Renderer(s0, W, H)
-    for f in range(3):
-        a = r1.tick_host(spp=spp, depth=depth, frame=f)
-        b = r0.tick_host(spp=spp, depth=depth, frame=f)
-        assert np.array_equal(a, b), f"frame {f}: {(a != b).sum()} pixels differ"
-    assert_acc_bits(r1.accumulator(), r0.accumulator())
-    assert r1.counters() == r0.counters()
 
 
 @pytest.mark.gpu

@@ -35,11 +35,6 @@ for s in "$@"; do
             for k in 4 8; do
                 step shard_mig_p$k 300 env GPU_MAX_HW_QUEUES=8 RT_SPLIT_PARTS=$k python tools/shard_time.py --scene mig16 --strong --deal balanced --out gpurun_out/shard_time_parts$k.jsonl
             done ;;
-        ptsplit)   # split bounce levels (RT_PT_SPLIT): parity, then A/B against the lane machine
-            step ptsplit_tests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread -k "split_levels or wavefront_equals" -s
-            step ptsplit_cfg5 400 python tools/knob_ab.py --scene cfg5 --spp 16 --depth 10 --var RT_PT_SPLIT=0 --var RT_PT_SPLIT=1 --rounds 5 --frames 3 --warm 3 --check --out gpurun_out/ptsplit_ab.jsonl
-            step ptsplit_cfg3 300 python tools/knob_ab.py --scene cfg3 --spp 4 --depth 4 --var RT_PT_SPLIT=0 --var RT_PT_SPLIT=1 --check --out gpurun_out/ptsplit_ab.jsonl
-            step ptsplit_tp 300 python tools/knob_ab.py --scene teapotF --spp 1 --depth 10 --var RT_PT_SPLIT=0 --var RT_PT_SPLIT=1 --check --out gpurun_out/ptsplit_ab.jsonl ;;
         region) step region 300 python tools/timed_region.py --out gpurun_out/timed_region.jsonl ;;
         parity4)   # round 4: the forced wave walk at full size, bit-exact accumulators, the deal machinery
             step parity4 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "wave_walk_config4 or baseline_configs or zero_seed or packet or primary_plus_shadow" -s ;;

@@ -78,7 +78,7 @@ struct rt_scene {
                                     // 2-7; 0 = frames in flight + 1)
     int32_t ps_pipeline = -1;       // primary+shadow frames overlap: -1 timed per renderer (auto),
                                     // 0 never, 1 always (RT_PS_PIPELINE)
-    uint32_t ps_depth = 2;          // frames in flight when forced (RT_PS_DEPTH, 2-6)
+    uint32_t ps_depth = 2;          // frames in flight when forced (RT_PS_DEPTH, 2-8)
     float tune_delay_ms = 100.0f;   // GPU time a parameter set runs before its timed choices start
                                     // (RT_TUNE_DELAY_MS): the clocks ramp over ~0.1 s, and choices
                                     // timed on the first frames at low clocks came out wrong
@@ -91,7 +91,7 @@ struct rt_scene {
 
 // frames in flight of overlapped primary+shadow frames: up to 6 renderer streams (with the
 // caller's and a communicator's stream, 8 = the bench's GPU_MAX_HW_QUEUES)
-constexpr int kPsMaxDepth = 6;
+constexpr int kPsMaxDepth = 8;   // renderer streams (frames in flight when forced: RT_PS_DEPTH)
 constexpr int kPtMaxSlots = 4;    // path-state slots of pipelined path-traced frames (RT_PT_SLOTS; <= kPsMaxDepth streams)
 
 struct rt_renderer {
@@ -108,6 +108,8 @@ struct rt_renderer {
     // maps while the camera walk is being timed), longest tile first afterwards
     uint32_t *d_order = nullptr, *d_cost = nullptr;
     std::vector<uint32_t> host_cost;   // the cost map the active order was sorted from (local tiles)
+    bool tail_bound = false;    // that map's costliest tile outlasts 2 x the frame's mean time per
+                                // resident wave slot: frames in flight beyond 2 become candidates
     uint32_t order_n = 0;
     uint64_t order_key = 0;
     int order_state = 0;        // 0 idle, 1 costs recorded, 2 order active, 3 costs held without an
@@ -955,6 +957,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
         r->order_key = key;
         r->order_state = 0;
         r->host_cost.clear();
+        r->tail_bound = false;
         r->ps_phase = 0;   // the overlap decision belongs to the parameter set too
         if (n != r->order_n) {
             HIP_TRY(hipDeviceSynchronize());                             // frames may still read them
@@ -985,6 +988,14 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
         std::vector<uint32_t> cost(n), ord(n);
         HIP_TRY(hipMemcpy(cost.data(), r->d_cost + (size_t)use * n, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
         r->host_cost = cost;
+        {   // a tile's cost is its wave's residence time, so sum / slots is the frame's throughput
+            // time and the costliest tile its latency floor (mig29 x16 1080p: 3.6x, its 1/2 shard
+            // 7x; TEAPOT-F 1080p 1.2-1.3x)
+            double sum = 0, mx = 0;
+            for (uint32_t c : cost) { sum += c; mx = std::max<double>(mx, c); }
+            const double slots = (double)r->scene->num_cus * 4.0 * 7.0;
+            r->tail_bound = sum > 0 && mx * slots > 2.0 * sum;
+        }
         for (uint32_t i = 0; i < n; ++i) ord[i] = i;
         std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
 
@@ -1281,10 +1292,13 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     uint32_t depth_k = (ps_ok && s->ps_pipeline == 1) ? s->ps_depth : 0u;
     int ps_ev0 = -1, ps_ev1 = -1;   // pev recorded on the caller's stream before / after this frame
     // More than 2 frames in flight are candidates only for frames of a few rounds of resident
-    // waves (a multi-GPU rank's small shard, 720p); a throughput-bound frame (TEAPOT-F 1080p, 8
-    // rounds) lost with 4 (0.1035 -> 0.114 ms) and the timing only risked picking them.  Groups
-    // in palindromic order: serial, 2, 4, 6, 6, 4, 2, serial -- or serial, 2, 2, serial.
-    const bool deep_ok = F.nunits <= 3u * 4u * 5u * s->num_cus;
+    // waves (a multi-GPU rank's small shard, 720p) or whose costliest tile outlasts twice the
+    // frame's throughput time (tail_bound, from the tile-order cost map: mig29 x16 1080p and its
+    // 1/2 shard, 16,200 tiles, 0.222 -> 0.167 ms with 4 in flight; round 4, depth_exp_*.jsonl);
+    // a throughput-bound frame (TEAPOT-F 1080p, 8 rounds) lost with 4 (0.1035 -> 0.114 ms) and
+    // the timing only risked picking them.  Groups in palindromic order: serial, 2, 4, 6, 6, 4,
+    // 2, serial -- or serial, 2, 2, serial.
+    const bool deep_ok = F.nunits <= 3u * 4u * 5u * s->num_cus || r->tail_bound;
     static const uint32_t kDeep[8] = {0, 2, 4, 6, 6, 4, 2, 0}, kShallow[4] = {0, 2, 2, 0};
     if (ps_ok && s->ps_pipeline < 0 && !gate_open) depth_k = 0;   // timing not started: serial
     if (ps_ok && s->ps_pipeline < 0 && gate_open) {
@@ -1296,14 +1310,14 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         if (r->ps_phase > 0 && r->ps_phase == NG * G) {
             HIP_TRY(hipEventSynchronize(r->pev[2 * NG - 1]));
             for (int g = 0; g < NG; ++g) HIP_TRY(hipEventElapsedTime(&r->ps_ms[g], r->pev[2 * g], r->pev[2 * g + 1]));
-            // group g and its mirror NG - 1 - g ran the same depth; frames in flight replace the
-            // serial frames (g = 0) only when they beat them by kTuneMargin (tuned_alternative)
-            const float serial = r->ps_ms[0] + r->ps_ms[NG - 1];
-            float best = serial;
+            // group g and its mirror NG - 1 - g ran the same depth; a depth replaces the
+            // shallower one chosen so far (serial first) only when it beats it by kTuneMargin
+            // (tuned_alternative), so noise does not buy frames in flight
+            float best = r->ps_ms[0] + r->ps_ms[NG - 1];
             r->ps_use = depths[0];
             for (int g = 1; g < NG / 2; ++g) {
                 const float t = r->ps_ms[g] + r->ps_ms[NG - 1 - g];
-                if (t < best && t < serial * (1.0f - kTuneMargin)) { best = t; r->ps_use = depths[g]; }
+                if (t < best * (1.0f - kTuneMargin)) { best = t; r->ps_use = depths[g]; }
             }
             r->ps_phase = -1;
             // every timed frame's finishing pass preceded pev[2 NG - 1]: no buffer is in use, and

@@ -85,6 +85,13 @@ def main():
     r0.close()
     ns = [int(x) for x in a.ns.split(",")]
     full_cost = None
+    if "balanced" in a.deal.split(",") and "interleaved" not in a.deal.split(","):
+        # the balanced deal cuts the measured cost map of a whole frame: measure it first
+        spp = a.spp if a.strong else a.spp * ns[0]
+        buf = torch.zeros(((a.w + 7) // 8) * ((a.h + 7) // 8) * 64, dtype=torch.int32, device="cuda")
+        _, cost = time_share(scene, a, spp, 4, lambda r, spp_, fr, s: r.render_shard(buf, 0, 1, spp=spp_, depth=a.depth,
+                                                                                      frame=fr, stream=s))
+        full_cost = cost.astype(np.uint32)
     res = {}
     for deal in a.deal.split(","):
         out = {}

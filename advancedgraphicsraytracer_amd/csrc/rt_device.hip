@@ -61,7 +61,7 @@ struct rt_scene {
     bool pt_dynamic = true;         // wavefront levels >= 1 fetch chunks dynamically (RT_PT_DYNAMIC=0: static)
     bool pt_wavefront = true;   // depth >= 2 path tracing: wavefront (k_pt_level) vs one kernel (k_render)
     uint32_t pt_drain_level = 64;   // bounce level from which the wavefront always drains (64 = never forced)
-    double pt_drain_rounds = 1.0;   // ... and it drains any level holding <= this many rounds of resident lanes
+    double pt_drain_rounds = 0.25;  // ... and it drains any level holding <= this many rounds of resident lanes
     bool tile_order = true;         // measured-cost (longest first) tile order (RT_TILE_ORDER=0: off)
     uint32_t split_units = 40000;   // sample split below this many tiles (1080p = 32,400 tiles)
     bool xcd_order = false;         // measured order grouped by XCD: blocks b, b + 8, ... (one XCD) render
@@ -72,7 +72,8 @@ struct rt_scene {
     uint64_t pt_mem_bytes = 12288ull << 20;   // path-state budget per slot (two when pipelined): 12 GB
                                               // of the 288 GB HBM holds all 16 spp of a 1080p depth-10 frame
     bool pt_pipeline = true;        // sample batches alternate path-state slots and streams
-    uint32_t pt_slots = 4;          // path-state slots / streams of pipelined frames (RT_PT_SLOTS, 2-4)
+    uint32_t pt_slots = 0;          // path-state slots / streams of pipelined frames (RT_PT_SLOTS, 2-8;
+                                    // 0 = 8 for batches of <= 8.4 M paths, else 4)
                                     // (RT_PT_PIPELINE=0: one slot, the caller's stream)
     uint32_t ps_buffers = 0;        // per-sample result buffers of overlapped frames (RT_PS_BUFFERS,
                                     // 2-7; 0 = frames in flight + 1)
@@ -92,7 +93,7 @@ struct rt_scene {
 // frames in flight of overlapped primary+shadow frames: up to 6 renderer streams (with the
 // caller's and a communicator's stream, 8 = the bench's GPU_MAX_HW_QUEUES)
 constexpr int kPsMaxDepth = 8;   // renderer streams (frames in flight when forced: RT_PS_DEPTH)
-constexpr int kPtMaxSlots = 4;    // path-state slots of pipelined path-traced frames (RT_PT_SLOTS; <= kPsMaxDepth streams)
+constexpr int kPtMaxSlots = 8;    // path-state slots of pipelined path-traced frames (RT_PT_SLOTS; <= kPsMaxDepth streams)
 
 struct rt_renderer {
     rt_scene *scene = nullptr;
@@ -773,7 +774,11 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
             HIP_TRY(hipMemGetInfo(&free_b, &total_b));
             double avail = (double)free_b;
             for (size_t b : r->pt_bytes) avail += (double)b;
-            uint32_t k = s->pt_slots;
+            // a frame of a few M paths (a multi-GPU rank's 1/8 of config 5: 4.1 M) is as long as
+            // its deep paths' latency chain, and 8 frames in flight overlap more of it (1/8 shard
+            // 1.24 -> 1.16-1.18 ms); whole 1080p x 16 spp frames lose with more than 4 (7.51 ->
+            // 7.61 / 7.72 ms with 6 / 8; profiles/r04/slots)
+            uint32_t k = s->pt_slots ? s->pt_slots : (np <= (8400u << 10) ? 8u : 4u);
             while (k > 2 && (double)k * need + (8ull << 30) > avail) --k;
             for (uint32_t j = k; j < (uint32_t)kPtMaxSlots; ++j) {
                 if (r->d_pt[j]) HIP_TRY(hipFree(r->d_pt[j]));

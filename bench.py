@@ -241,15 +241,18 @@ def main():
     frame_out = torch.zeros(W * H, dtype=torch.int32, device=f"cuda:{device}")
     sharded = None
     native_fallback = None
+    balanced_deal = args.scaling == "strong" and args.depth == 1
     if world > 1:
         from advancedgraphicsraytracer_amd.distributed import NativeCommUnavailable, NativeShardedFrame, ShardedFrame
         if backend == "nccl":   # the product path: RCCL gather from C++ (rt_render_frame_multi)
-            # strong scaling renders compact cost-balanced screen regions per rank from a parameter
-            # set's 7th frame on (RT_MULTI_BALANCED: each GPU's caches hold its region's part of
-            # the scene); weak scaling keeps the interleaved deal, whose 1/N shards at spp N are
-            # statistically identical (tools/shard_time.py)
+            # strong-scaling primary+shadow frames (config 4) render compact cost-balanced screen
+            # regions per rank once the costs are measured (RT_MULTI_BALANCED: each GPU's caches
+            # hold its region's part of the scene); weak scaling keeps the interleaved deal, whose
+            # 1/N shards at spp N are statistically identical, and so do path-traced frames: the
+            # level-0 cost deal measured slower than interleaving on config 5 (1/8 shard 1.56 vs
+            # 1.31 ms, the bounce levels' cost is not the camera rays')
             try:
-                sharded = NativeShardedFrame(rend, device=torch.device("cuda", device), balanced=args.scaling == "strong")
+                sharded = NativeShardedFrame(rend, device=torch.device("cuda", device), balanced=balanced_deal)
             except NativeCommUnavailable as e:   # raised on every rank together: same gather via torch's RCCL
                 if rank == 0:
                     print(f"bench: native RCCL communicator unavailable ({e}); torch.distributed gather instead",
@@ -347,7 +350,7 @@ def main():
             dist.all_reduce(per, op=dist.ReduceOp.MAX)
             di = sharded.deal_info()   # the deal this rank's frames actually ran under
             multi = {"exchange": "rt_render_frame_multi (RCCL send/recv to rank 0 from C++, pipelined)",
-                     "deal_requested": "balanced (RT_MULTI_BALANCED)" if args.scaling == "strong" else "interleaved t % N",
+                     "deal_requested": "balanced (RT_MULTI_BALANCED)" if balanced_deal else "interleaved t % N",
                      "deal_rank0": {"in_use": "balanced" if di["balanced"] else "interleaved", **di},
                      "render_ms_per_frame_max_rank": round(per[0].item(), 4),
                      "gather_ms_per_frame_max_rank": round(per[1].item(), 4)}

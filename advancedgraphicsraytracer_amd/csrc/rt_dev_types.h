@@ -73,6 +73,11 @@ struct FrameArgs {
     uint32_t *out;
     unsigned long long *counters;       // kCounterSlots slots of 8 u64 (64 B): [0] shadow rays, [1] bounce rays
                                         // ([2..5] the camera walk's counters, SceneView::walk_stats)
+    // short LDS stacks (the 8-wave frame kernel on deep trees): entries [0, lds_entries) of a
+    // lane's traversal stack in LDS, deeper ones at stack_ovf[(i - lds_entries) * ovf_lanes +
+    // unit * 64 + lane]; lds_entries = 0: the whole stack in LDS
+    uint32_t lds_entries, ovf_lanes;
+    uint32_t *stack_ovf;
 };
 
 // One launch of the frame kernel family (Renderer::Tick): integrator mode, Trace depth
@@ -84,6 +89,7 @@ struct FrameLaunch {
     dim3 grid, block;
     size_t lds_bytes;
     hipStream_t stream;
+    int waves;       // primary+shadow frames: 8 = the 8-waves/SIMD build (k_render_w8), else the plain one
 };
 
 // Wavefront path tracing (RT_MODE_PATH, Trace depth >= 2): the frame's paths advance one
@@ -138,6 +144,7 @@ struct TraceArgs {
 #define RT_DECLARE_LAUNCHERS(NS)                                                                  \
     namespace NS {                                                                                \
     void launch_frame(const SceneView &S, const FrameArgs &F, const FrameLaunch &L);              \
+    int frame_w8_blocks(bool tex, size_t lds);                                                    \
     void launch_intersect(const SceneView &S, const rt_ray *rays, rt_hit *hits, uint32_t n,       \
                           size_t lds, hipStream_t st);                                            \
     void launch_occluded(const SceneView &S, const rt_ray *rays, uint8_t *out, uint32_t n,        \

@@ -74,9 +74,9 @@ import roofline as rl  # noqa: E402
 # BASELINE.json configs[1..4]: scene recipe, spp, Trace depth, N > 1 scaling,
 # dominant kernel (the roofline's subject; profiles/pmc_summary.json key cfgN)
 CONFIGS = {
-    2: dict(scene="teapotF", spp=1, depth=1, scaling="weak", kernel="k_render<0, 1, false>"),
+    2: dict(scene="teapotF", spp=1, depth=1, scaling="weak", kernel="k_render"),
     3: dict(scene="cfg3", spp=4, depth=4, scaling="weak", kernel="k_pt_lanes"),
-    4: dict(scene="mig16", spp=1, depth=1, scaling="strong", kernel="k_render<0, 1, false>"),
+    4: dict(scene="mig16", spp=1, depth=1, scaling="strong", kernel="k_render"),
     5: dict(scene="cfg5", spp=16, depth=10, scaling="strong", kernel="k_pt_lanes"),
 }
 # Algorithmic bytes per ray, SURVEY.md 8(d): B = 32*A + 40*P (+36 B pixel IO per camera

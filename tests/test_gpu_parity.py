@@ -723,6 +723,34 @@ def test_split_parts_keep_frames(rt, torch, monkeypatch, recipe, shards, parts):
     assert ra.counters() == rb.counters()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("recipe,W,H,spp", [("teapotF", 1920, 1080, 1), ("mig16", 640, 360, 1), ("cfg3", 320, 180, 2),
+                                            ("cfg5", 320, 180, 4)])
+def test_frame_kernel_builds_agree(rt, torch, monkeypatch, recipe, W, H, spp):
+    """The primary+shadow frame kernel's 8-waves/SIMD build (k_render_w8: 64 VGPRs, spilling),
+    with full or short LDS stacks (RT_STACK_SHORT; RT_STACK_LDS=3 sends most pushes to the
+    global overflow, the wave walk's uniform stack included), and its plain build
+    (RT_FRAME_WAVES=8 / 7) give the same frames, accumulator bits and ray counts over 6 frames,
+    a reset included; RT_FRAME_WAVES=0 (the default) picks one of them."""
+    variants = {"plain": {"RT_FRAME_WAVES": "7"}, "w8": {"RT_FRAME_WAVES": "8"}, "auto": {},
+                "short": {"RT_STACK_SHORT": "1"}, "short3": {"RT_FRAME_WAVES": "8", "RT_STACK_LDS": "3"}}
+    scenes = {}
+    for name, env in variants.items():
+        for k in ("RT_FRAME_WAVES", "RT_STACK_SHORT", "RT_STACK_LDS"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        scenes[name] = rt.Scene.recipe(recipe)
+    rs = {w: rt.Renderer(sc, W, H) for w, sc in scenes.items()}
+    for f in range(6):
+        outs = {w: r.tick_host(spp=spp, depth=1, frame=f, reset=(f == 3)) for w, r in rs.items()}
+        for w in variants:
+            assert np.array_equal(outs[w], outs["plain"]), f"{w} frame {f}: {(outs[w] != outs['plain']).sum()} px"
+    for w in variants:
+        assert_acc_bits(rs[w].accumulator(), rs["plain"].accumulator())
+        assert rs[w].counters() == rs["plain"].counters()
+
+
 # ---- BASELINE.json configs at their full size against the oracle
 @pytest.mark.parametrize("recipe,W,H,spp,depth,frames", [
     ("teapotF", 3840, 2160, 1, 1, 5),     # 4K, past the walk timing and the tile-order switch (frame 4)

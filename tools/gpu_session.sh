@@ -49,7 +49,8 @@ for s in "$@"; do
             # so their trace durations would not be one kernel's; no 720p companion run (same kernel name)
             export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0
             for c in ${PROF_CONFIGS:-2 3 4 5}; do
-                if [ $c = 2 ] || [ $c = 4 ]; then n=60; k="k_render<0, 1, false>"; else n=6; k="k_pt_lanes"; fi
+                # k_render: the plain build (k_render<0, 1, false>) or the 8-wave one (k_render_w8<false>)
+                if [ $c = 2 ] || [ $c = 4 ]; then n=60; k="k_render"; else n=6; k="k_pt_lanes"; fi
                 b="python bench.py --config $c --steps $n --warmup 2 --no-cpu-baseline --no-companion --ramp-seconds 0.3"
                 step prof_c$c 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pc$c/trace -o run --output-format csv -- $b
                 step pmc_c${c}_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pc$c/fetch -o pmc --output-format csv -- $b

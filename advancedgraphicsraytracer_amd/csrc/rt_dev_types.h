@@ -73,11 +73,6 @@ struct FrameArgs {
     uint32_t *out;
     unsigned long long *counters;       // kCounterSlots slots of 8 u64 (64 B): [0] shadow rays, [1] bounce rays
                                         // ([2..5] the camera walk's counters, SceneView::walk_stats)
-    // short LDS stacks (the 8-wave frame kernel on deep trees): entries [0, lds_entries) of a
-    // lane's traversal stack in LDS, deeper ones at stack_ovf[(i - lds_entries) * ovf_lanes +
-    // unit * 64 + lane]; lds_entries = 0: the whole stack in LDS
-    uint32_t lds_entries, ovf_lanes;
-    uint32_t *stack_ovf;
 };
 
 // One launch of the frame kernel family (Renderer::Tick): integrator mode, Trace depth

@@ -53,11 +53,9 @@ struct rt_scene {
     Bvh bvh;
     uint32_t num_prims = 0;
     uint32_t stack_depth = 0;   // LDS stack entries per lane
-    int frame_waves = 0;        // primary+shadow frame kernel build: 0 = the 8-waves/SIMD build where
-                                // 8 workgroups fit beside the LDS stacks (short stacks: see
-                                // short_stack), else the plain one (RT_FRAME_WAVES=7/8 force)
-    bool short_stack = false;   // 8-wave build on deep trees with short LDS stacks + global overflow (RT_STACK_SHORT)
-    uint32_t short_max = 64;    // ... at most this many of their entries in LDS (RT_STACK_LDS; tests force the overflow)
+    int frame_waves = 0;        // primary+shadow frame kernel build: 0 = the 8-waves/SIMD build for serial
+                                // frames where 8 workgroups fit beside the LDS stacks, else the plain
+                                // one (RT_FRAME_WAVES=7 / 8 force one where it fits)
     uint32_t num_cus = 256;     // persistent grid size of k_render_lds
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
     int walk = RT_WALK_LANE;    // camera-ray walk of the global-node primary+shadow kernel
@@ -149,10 +147,7 @@ struct rt_renderer {
     // renderer streams: the path tracer's two path streams are 0 and 1; overlapped primary+
     // shadow frames use the first `depth` of them (frames in flight)
     hipStream_t pt_stream[kPsMaxDepth] = {};
-    // short-stack overflow of the 8-wave frame kernel, one per stream a frame kernel runs on
-    // (the renderer streams, then the caller's): frames on one stream run one after another
-    uint32_t *d_ovf[kPsMaxDepth + 1] = {};
-    size_t ovf_bytes[kPsMaxDepth + 1] = {};
+
     hipEvent_t pt_lv[kPsMaxDepth] = {};   // a renderer stream's work of this frame is done
     hipEvent_t pt_fin[kPtMaxSlots + 1] = {};   // the finish that read d_res[b] is done
     bool pt_fin_set[kPtMaxSlots + 1] = {};
@@ -599,8 +594,6 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_TILE_ORDER")) s->tile_order = std::atoi(e) != 0;
     // RT_SPLIT_UNITS: sample-split target units (0 = never split)
     if (const char *e = std::getenv("RT_SPLIT_UNITS")) s->split_units = (uint32_t)std::max(0, std::atoi(e));
-    if (const char *e = std::getenv("RT_STACK_SHORT")) s->short_stack = std::atoi(e) != 0;
-    if (const char *e = std::getenv("RT_STACK_LDS")) s->short_max = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_FRAME_WAVES")) {
         const int w = std::atoi(e);
         s->frame_waves = w == 7 || w == 8 ? w : 0;
@@ -969,44 +962,17 @@ std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const uint32_t *map,
     return out;
 }
 
-// The primary+shadow frame kernel's build (FrameLaunch::waves).  The 8-waves/SIMD build runs
-// where 8 of its workgroups fit on a CU beside their LDS stacks (TEAPOT-F: 15 entries); on a
-// deeper tree (mig29 x16: 26 entries, 6 workgroups) it runs with short stacks -- the first
-// entries that let 8 fit in LDS, the rest in this stream's overflow buffer -- when short_stack
-// is set or the build is forced, and the plain 7-wave build otherwise.  slot: the stream's
-// overflow buffer (renderer stream k, kPsMaxDepth = the caller's).
-int frame_build(rt_renderer *r, const SceneView &view, FrameArgs &F, FrameLaunch &L, int slot) {
+// The primary+shadow frame kernel's build (FrameLaunch::waves): the 8-waves/SIMD build for
+// serial frames where 8 of its workgroups fit on a CU beside their LDS stacks (TEAPOT-F: 15
+// entries; mig29 x16: 26 entries, 6 fit), the plain 7-wave build otherwise (k_render_w8).
+void frame_build(const rt_renderer *r, const SceneView &view, FrameLaunch &L, bool overlapped) {
     const rt_scene *s = r->scene;
-    F.lds_entries = 0;
-    F.stack_ovf = nullptr;
-    F.ovf_lanes = 0;
     L.waves = 7;
-    if (L.mode != RT_MODE_PATH || L.md != 1 || s->frame_waves == 7) return RT_OK;
-    if (view.wave_primary && view.walk_check != RT_WALK_CHECK_OFF) return RT_OK;   // the walk-check build
-    auto blocks = [&](size_t lds) {
-        return s->ext ? kext::frame_w8_blocks(L.tex, lds) : kcore::frame_w8_blocks(L.tex, lds);
-    };
-    const bool forced_short = s->short_max < s->stack_depth;
-    if (blocks(L.lds_bytes) >= 8 && !forced_short) { L.waves = 8; return RT_OK; }
-    if (!s->short_stack && s->frame_waves != 8 && !forced_short) return RT_OK;
-    uint32_t k = std::min(s->stack_depth, s->short_max);
-    while (k > 1 && blocks((size_t)k * 256u * sizeof(uint32_t)) < 8) --k;
-    const uint64_t lanes = (uint64_t)F.nunits * 64u;
-    const size_t need = (size_t)(lanes * (s->stack_depth - k) * sizeof(uint32_t));
-    if (need > r->ovf_bytes[slot]) {
-        HIP_TRY(hipStreamSynchronize(L.stream));   // the stream's earlier frames are done with it
-        if (r->d_ovf[slot]) HIP_TRY(hipFree(r->d_ovf[slot]));
-        r->d_ovf[slot] = nullptr;
-        r->ovf_bytes[slot] = 0;
-        HIP_TRY(hipMalloc(&r->d_ovf[slot], need));
-        r->ovf_bytes[slot] = need;
-    }
-    F.lds_entries = k;
-    F.ovf_lanes = (uint32_t)lanes;
-    F.stack_ovf = r->d_ovf[slot];
-    L.lds_bytes = (size_t)k * 256u * sizeof(uint32_t);
-    L.waves = 8;
-    return RT_OK;
+    if (L.mode != RT_MODE_PATH || L.md != 1 || s->frame_waves == 7) return;
+    if (view.wave_primary && view.walk_check != RT_WALK_CHECK_OFF) return;   // the walk-check build
+    if (overlapped && s->frame_waves != 8) return;
+    const int blocks = s->ext ? kext::frame_w8_blocks(L.tex, L.lds_bytes) : kcore::frame_w8_blocks(L.tex, L.lds_bytes);
+    if (blocks >= 8) L.waves = 8;
 }
 
 int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, bool split_ok, bool gate_open,
@@ -1435,7 +1401,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         F.samples = r->ps_res[buf];
     }
     if (ps_ok) r->ps_prev = depth_k;
-    if (int rc = frame_build(r, view, F, L, ps_pipe ? lane_st : kPsMaxDepth); rc != RT_OK) return rc;
+    frame_build(r, view, L, ps_pipe);
     if (walk_ev0 >= 0) HIP_TRY(hipEventRecord(r->tev[walk_ev0], st));
     if (split_ev0 >= 0) HIP_TRY(hipEventRecord(r->sev[split_ev0], st));
     if (s->ext) kext::launch_frame(view, F, L);
@@ -1756,8 +1722,6 @@ int rt_renderer_destroy(rt_renderer *r) {
         if (r->pt_stream[k]) (void)hipStreamDestroy(r->pt_stream[k]);
         if (r->pt_lv[k]) (void)hipEventDestroy(r->pt_lv[k]);
     }
-    for (uint32_t *p : r->d_ovf)
-        if (p) (void)hipFree(p);
     for (int k = 0; k <= kPtMaxSlots; ++k) {
         if (r->d_res[k]) (void)hipFree(r->d_res[k]);
         if (r->pt_fin[k]) (void)hipEventDestroy(r->pt_fin[k]);

@@ -727,17 +727,13 @@ def test_split_parts_keep_frames(rt, torch, monkeypatch, recipe, shards, parts):
 @pytest.mark.parametrize("recipe,W,H,spp", [("teapotF", 1920, 1080, 1), ("mig16", 640, 360, 1), ("cfg3", 320, 180, 2),
                                             ("cfg5", 320, 180, 4)])
 def test_frame_kernel_builds_agree(rt, torch, monkeypatch, recipe, W, H, spp):
-    """The primary+shadow frame kernel's 8-waves/SIMD build (k_render_w8: 64 VGPRs, spilling),
-    with full or short LDS stacks (RT_STACK_SHORT; RT_STACK_LDS=3 sends most pushes to the
-    global overflow, the wave walk's uniform stack included), and its plain build
-    (RT_FRAME_WAVES=8 / 7) give the same frames, accumulator bits and ray counts over 6 frames,
-    a reset included; RT_FRAME_WAVES=0 (the default) picks one of them."""
-    variants = {"plain": {"RT_FRAME_WAVES": "7"}, "w8": {"RT_FRAME_WAVES": "8"}, "auto": {},
-                "short": {"RT_STACK_SHORT": "1"}, "short3": {"RT_FRAME_WAVES": "8", "RT_STACK_LDS": "3"}}
+    """The primary+shadow frame kernel's 8-waves/SIMD build (k_render_w8: 64 VGPRs, spilling)
+    and its plain build (RT_FRAME_WAVES=8 / 7) give the same frames, accumulator bits and ray
+    counts over 6 frames, a reset included; RT_FRAME_WAVES=0 (the default) picks one of them."""
+    variants = {"plain": {"RT_FRAME_WAVES": "7"}, "w8": {"RT_FRAME_WAVES": "8"}, "auto": {}}
     scenes = {}
     for name, env in variants.items():
-        for k in ("RT_FRAME_WAVES", "RT_STACK_SHORT", "RT_STACK_LDS"):
-            monkeypatch.delenv(k, raising=False)
+        monkeypatch.delenv("RT_FRAME_WAVES", raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         scenes[name] = rt.Scene.recipe(recipe)

@@ -101,10 +101,20 @@ def main():
             buf = torch.zeros(cap, dtype=torch.int32, device="cuda")
             if deal == "balanced":
                 tiles, off = rt.tile_deal(a.w, a.h, n, full_cost if (full_cost is not None and full_cost.size) else None)
+            elif deal.startswith("blocks"):   # blocksB: BxB-tile blocks dealt round-robin (block b -> rank b % n)
+                B = int(deal[6:] or 8)
+                tx, ty = (a.w + 7) // 8, (a.h + 7) // 8
+                t = np.arange(tx * ty)
+                bx, by = (t % tx) // B, (t // tx) // B
+                blk = by * ((tx + B - 1) // B) + bx
+                owner = blk % n
+                order = np.lexsort((t, blk))
+                tiles = np.concatenate([order[owner[order] == k] for k in range(n)]).astype(np.uint32)
+                off = np.concatenate([[0], np.cumsum([(owner == k).sum() for k in range(n)])]).astype(np.int64)
             ranks = range(n) if a.ranks == "all" else [n - 1]
             per = []
             for k in ranks:
-                if deal == "balanced":
+                if deal == "balanced" or deal.startswith("blocks"):
                     mine = tiles[off[k]:off[k + 1]]
                     render = lambda r, spp_, fr, s, mine=mine: r.render_shard_tiles(buf, mine, spp=spp_, depth=a.depth, frame=fr, stream=s)
                 else:

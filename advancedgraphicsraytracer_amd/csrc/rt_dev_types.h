@@ -84,7 +84,7 @@ struct FrameLaunch {
     dim3 grid, block;
     size_t lds_bytes;
     hipStream_t stream;
-    int waves;       // primary+shadow frames: 8 = the 8-waves/SIMD build (k_render_w8), else the plain one
+    int waves;       // primary+shadow frames: 8 = the single-sample build (k_render_w8), else the plain one
 };
 
 // Wavefront path tracing (RT_MODE_PATH, Trace depth >= 2): the frame's paths advance one
@@ -139,7 +139,6 @@ struct TraceArgs {
 #define RT_DECLARE_LAUNCHERS(NS)                                                                  \
     namespace NS {                                                                                \
     void launch_frame(const SceneView &S, const FrameArgs &F, const FrameLaunch &L);              \
-    int frame_w8_blocks(bool tex, size_t lds);                                                    \
     void launch_intersect(const SceneView &S, const rt_ray *rays, rt_hit *hits, uint32_t n,       \
                           size_t lds, hipStream_t st);                                            \
     void launch_occluded(const SceneView &S, const rt_ray *rays, uint8_t *out, uint32_t n,        \

@@ -53,10 +53,9 @@ struct rt_scene {
     Bvh bvh;
     uint32_t num_prims = 0;
     uint32_t stack_depth = 0;   // LDS stack entries per lane
-    int frame_waves = 0;        // primary+shadow frame kernel build: 0 = the 8-waves/SIMD build for serial
-                                // frames where 8 workgroups fit beside the LDS stacks, else the plain
-                                // one (RT_FRAME_WAVES=7 / 8 force one where it fits)
-    uint32_t num_cus = 256;     // persistent grid size of k_render_lds
+    int frame_waves = 0;        // primary+shadow frame kernel build (frame_build): 0 = chosen, 7 = the
+                                // plain build, 8 = the single-sample one wherever it applies (RT_FRAME_WAVES)
+    uint32_t num_cus = 256;     // CUs of the device (resident grids, frames-in-flight rules)
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
     int walk = RT_WALK_LANE;    // camera-ray walk of the global-node primary+shadow kernel
     bool ext = false;           // needs the kext kernels (cubes, quads, textures, non-Light light)
@@ -962,17 +961,21 @@ std::vector<uint32_t> xcd_grouped_order(const FrameArgs &F, const uint32_t *map,
     return out;
 }
 
-// The primary+shadow frame kernel's build (FrameLaunch::waves): the 8-waves/SIMD build for
-// serial frames where 8 of its workgroups fit on a CU beside their LDS stacks (TEAPOT-F: 15
-// entries; mig29 x16: 26 entries, 6 fit), the plain 7-wave build otherwise (k_render_w8).
-void frame_build(const rt_renderer *r, const SceneView &view, FrameLaunch &L, bool overlapped) {
+// The primary+shadow frame kernel's build (FrameLaunch::waves): frames of one sample per work
+// unit run k_render_w8 (render_tile ONE: no sample loop, 51 VGPRs, 8 waves/SIMD where the LDS
+// stacks allow), others the plain k_render (71 VGPRs, 7 waves).
+void frame_build(const rt_renderer *r, const SceneView &view, const FrameArgs &F, FrameLaunch &L, bool overlapped) {
     const rt_scene *s = r->scene;
     L.waves = 7;
     if (L.mode != RT_MODE_PATH || L.md != 1 || s->frame_waves == 7) return;
+    if (F.nchunks != std::max(1u, F.spp)) return;   // the 8-wave build traces one sample per unit
     if (view.wave_primary && view.walk_check != RT_WALK_CHECK_OFF) return;   // the walk-check build
-    if (overlapped && s->frame_waves != 8) return;
-    const int blocks = s->ext ? kext::frame_w8_blocks(L.tex, L.lds_bytes) : kcore::frame_w8_blocks(L.tex, L.lds_bytes);
-    if (blocks >= 8) L.waves = 8;
+    // small overlapped frames (<= 3 rounds of resident waves: TEAPOT-F 720p with 4 in flight
+    // 0.059 -> 0.062 ms) keep the plain build; everywhere else the single-sample build won or
+    // tied (TEAPOT-F 1080p serial 0.1025 -> 0.096, 2 in flight 0.108 -> 0.099; mig29 x16 1080p 4 in
+    // flight 0.223 -> 0.215, serial 0.466 -> 0.471; profiles/r04/frame_build/one_*.log)
+    if (overlapped && F.nunits <= 3u * 4u * 5u * s->num_cus && s->frame_waves != 8) return;
+    L.waves = 8;
 }
 
 int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, bool split_ok, bool gate_open,
@@ -1401,7 +1404,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         F.samples = r->ps_res[buf];
     }
     if (ps_ok) r->ps_prev = depth_k;
-    frame_build(r, view, L, ps_pipe);
+    frame_build(r, view, F, L, ps_pipe);
     if (walk_ev0 >= 0) HIP_TRY(hipEventRecord(r->tev[walk_ev0], st));
     if (split_ev0 >= 0) HIP_TRY(hipEventRecord(r->sev[split_ev0], st));
     if (s->ext) kext::launch_frame(view, F, L);

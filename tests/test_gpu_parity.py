@@ -727,9 +727,10 @@ def test_split_parts_keep_frames(rt, torch, monkeypatch, recipe, shards, parts):
 @pytest.mark.parametrize("recipe,W,H,spp", [("teapotF", 1920, 1080, 1), ("mig16", 640, 360, 1), ("cfg3", 320, 180, 2),
                                             ("cfg5", 320, 180, 4)])
 def test_frame_kernel_builds_agree(rt, torch, monkeypatch, recipe, W, H, spp):
-    """The primary+shadow frame kernel's 8-waves/SIMD build (k_render_w8: 64 VGPRs, spilling)
-    and its plain build (RT_FRAME_WAVES=8 / 7) give the same frames, accumulator bits and ray
-    counts over 6 frames, a reset included; RT_FRAME_WAVES=0 (the default) picks one of them."""
+    """The primary+shadow frame kernel's single-sample build (k_render_w8: no sample loop, 8
+    waves/SIMD; one sample per work unit -- spp 1, or the sample split at spp > 1) and its plain
+    build (RT_FRAME_WAVES=8 / 7) give the same frames, accumulator bits and ray counts over 6
+    frames, a reset included; RT_FRAME_WAVES=0 (the default) picks one of them."""
     variants = {"plain": {"RT_FRAME_WAVES": "7"}, "w8": {"RT_FRAME_WAVES": "8"}, "auto": {}}
     scenes = {}
     for name, env in variants.items():

@@ -1019,11 +1019,12 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
         r->host_cost = cost;
         {   // a tile's cost is its wave's residence time, so sum / slots is the frame's throughput
             // time and the costliest tile its latency floor (mig29 x16 1080p: 3.6x, its 1/2 shard
-            // 7x; TEAPOT-F 1080p 1.2-1.3x)
+            // 7x; TEAPOT-F 1080p 1.2-1.3x).  A sample-split frame's map holds one chunk's cycles
+            // per tile (the last unit of the tile to finish writes it): nchunks of them run.
             double sum = 0, mx = 0;
             for (uint32_t c : cost) { sum += c; mx = std::max<double>(mx, c); }
             const double slots = (double)r->scene->num_cus * 4.0 * 7.0;
-            r->tail_bound = sum > 0 && mx * slots > 2.0 * sum;
+            r->tail_bound = sum > 0 && mx * slots > 2.0 * sum * std::max(1u, F.nchunks);
         }
         for (uint32_t i = 0; i < n; ++i) ord[i] = i;
         std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
@@ -1081,7 +1082,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
     return RT_OK;
 }
 
-constexpr int kPsGroup = 8;   // frames per timed group of the overlap decision
+constexpr int kPsGroup = 16;  // frames per timed group of the overlap decision (8 in round 3)
 
 // the parameter set a frame belongs to (the tuned choices and the tile order are per set)
 uint64_t param_key(const rt_renderer *r, const FrameArgs &F, const rt_camera *cam, const rt_frame_params *p) {
@@ -1319,7 +1320,13 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
                        ps_bytes <= (2ull << 30);
     // frames in flight for this frame: 0 = serial, else 2..6 renderer streams
     uint32_t depth_k = (ps_ok && s->ps_pipeline == 1) ? s->ps_depth : 0u;
-    int ps_ev0 = -1, ps_ev1 = -1;   // pev recorded on the caller's stream before / after this frame
+    // pev recorded on the caller's stream after this frame: ps_ev0 after a timed group's first
+    // frame, ps_ev1 after its last -- the group is timed from one frame's completion to another's,
+    // G - 1 frame periods at its depth in steady state.  (Events before the first frame timed a
+    // deeper group short: its first kernels start on their streams while the caller's stream still
+    // finishes earlier frames; TEAPOT-F shards then picked 4-6 in flight, 0.125-0.144 ms against
+    // 0.092 with 2.  Round 4.)
+    int ps_ev0 = -1, ps_ev1 = -1;
     // More than 2 frames in flight are candidates only for frames of a few rounds of resident
     // waves (a multi-GPU rank's small shard, 720p) or whose costliest tile outlasts twice the
     // frame's throughput time (tail_bound, from the tile-order cost map: mig29 x16 1080p and its
@@ -1380,7 +1387,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         }
     }
     const bool ps_pipe = depth_k > 0;
-    if (ps_ev0 >= 0) HIP_TRY(hipEventRecord(r->pev[ps_ev0], st));
+
     uint32_t buf = 0;
     int lane_st = 0;
     if (ps_pipe) {
@@ -1428,6 +1435,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
             r->ps_fin_set[buf] = true;
         }
     }
+    if (ps_ev0 >= 0) HIP_TRY(hipEventRecord(r->pev[ps_ev0], st));
     if (ps_ev1 >= 0) HIP_TRY(hipEventRecord(r->pev[ps_ev1], st));
     (void)tiles_y;
     r->primary += frame_pixels(r, F, shard, nshards, tiles_x, ntiles) * p->spp;

@@ -968,7 +968,7 @@ void frame_build(const rt_renderer *r, const SceneView &view, const FrameArgs &F
     const rt_scene *s = r->scene;
     L.waves = 7;
     if (L.mode != RT_MODE_PATH || L.md != 1 || s->frame_waves == 7) return;
-    if (F.nchunks != std::max(1u, F.spp)) return;   // the 8-wave build traces one sample per unit
+    if (F.nchunks != std::max(1u, F.spp)) return;   // the single-sample build: one sample per unit
     if (view.wave_primary && view.walk_check != RT_WALK_CHECK_OFF) return;   // the walk-check build
     // small overlapped frames (<= 3 rounds of resident waves: TEAPOT-F 720p with 4 in flight
     // 0.059 -> 0.062 ms) keep the plain build; everywhere else the single-sample build won or

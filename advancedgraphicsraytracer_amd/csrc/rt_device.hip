@@ -1403,10 +1403,16 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         if ((rc = ensure_ps_res(r, buf, ps_bytes)) != RT_OK) return rc;
         L.stream = r->pt_stream[lane_st];
         if (r->ps_fin_set[buf]) HIP_TRY(hipStreamWaitEvent(L.stream, r->ps_fin[buf], 0));
-        if (!r->ps_prev) {   // switching from serial frames: start behind the caller's stream
+        if (!r->ps_prev || ps_ev0 >= 0) {
+            // switching from serial frames: start behind the caller's stream; a timed group's first
+            // frame: every renderer stream starts behind everything before it, so that no frame of
+            // the group runs beside the previous group's (whose depth differs)
             if (!r->ps_join) HIP_TRY(hipEventCreateWithFlags(&r->ps_join, hipEventDisableTiming | hipEventReleaseToDevice));
             HIP_TRY(hipEventRecord(r->ps_join, st));
-            HIP_TRY(hipStreamWaitEvent(L.stream, r->ps_join, 0));
+            if (ps_ev0 >= 0)
+                for (int k = 0; k < kPsMaxDepth; ++k) HIP_TRY(hipStreamWaitEvent(r->pt_stream[k], r->ps_join, 0));
+            else
+                HIP_TRY(hipStreamWaitEvent(L.stream, r->ps_join, 0));
         }
         F.samples = r->ps_res[buf];
     }

@@ -5,7 +5,7 @@ each round `--frames` back-to-back frames between two HIP events on one stream; 
 per-variant median and min ms/frame, and (--check) asserts every variant's last frame equals
 the first variant's bit for bit.
 
-usage: knob_ab.py --scene cfg5 --spp 16 --depth 10 --var RT_PT_SORT=0 --var RT_PT_SORT=3 [--var A=1,B=2]
+usage: knob_ab.py --scene cfg5 --spp 16 --depth 10 --var RT_PT_DRAIN_ROUNDS=1 --var RT_PT_DRAIN_ROUNDS=0.25 [--var A=1,B=2]
                   [--w 1920 --h 1080] [--rounds 7] [--frames 4] [--warm 6] [--check] [--out f.jsonl]"""
 import argparse
 import json

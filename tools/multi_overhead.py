@@ -27,6 +27,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scene", default="teapotF")
     ap.add_argument("--frames", type=int, default=300)
+    ap.add_argument("--warm", type=int, default=400, help="untimed frames first, per mode: past the renderer's "
+                    "timed choices (walk, split order, frames in flight: ~170 frames after the tuning gate) ...")
+    ap.add_argument("--warm-seconds", type=float, default=1.0, help="... and at least this much wall time (the "
+                    "tuning gate opens after 100 ms of GPU time, RT_TUNE_DELAY_MS)")
     ap.add_argument("--spp", type=int, default=1)
     ap.add_argument("--depth", type=int, default=1)
     ap.add_argument("--events", choices=("none", "plain", "bench"), default="plain",
@@ -46,19 +50,28 @@ def main():
     res = {}
     with torch.cuda.stream(st):
         sptr = st.cuda_stream
-        for _ in range(20):
+        w0, f = time.perf_counter(), 0
+        while f < a.warm or time.perf_counter() - w0 < a.warm_seconds:
             r.Tick(out, spp=a.spp, depth=a.depth, frame=0, stream=sptr)
+            f += 1
+            if f % 50 == 0:
+                st.synchronize()
         st.synchronize()
         t0 = time.perf_counter()
         for f in range(a.frames):
             r.Tick(out, spp=a.spp, depth=a.depth, frame=f, stream=sptr)
         st.synchronize()
         res["tick_ms"] = (time.perf_counter() - t0) * 1e3 / a.frames
+        res["tick_in_flight"] = r.overlap_depth()[0]
         sf = NativeShardedFrame(r, timing=False)
         ev = None if a.events == "none" else (torch.cuda.Event(enable_timing=a.events == "bench"),
                                                torch.cuda.Event(enable_timing=a.events == "bench"))
-        for f in range(20):
+        w0, f = time.perf_counter(), 0
+        while f < a.warm or time.perf_counter() - w0 < a.warm_seconds:
             sf.submit(spp=a.spp, depth=a.depth, frame=f, stream=sptr, events=ev)
+            f += 1
+            if f % 50 == 0:
+                st.synchronize()
         sf.flush(stream=sptr)
         st.synchronize()
         if a.events == "bench":
@@ -73,6 +86,8 @@ def main():
         st.synchronize()
         res["multi_submit_ms"] = (time.perf_counter() - t0) * 1e3 / a.frames
         res["multi_submit_host_ms"] = host * 1e3 / a.frames
+        res["multi_in_flight"] = r.overlap_depth()[0]
+        res["multi_choices"] = r.choices()
         sf.close()
     dist.destroy_process_group()
     res.update(scene=a.scene, spp=a.spp, depth=a.depth, frames=a.frames, events=a.events)

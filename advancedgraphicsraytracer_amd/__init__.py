@@ -152,6 +152,7 @@ def lib():
         "rt_comm_timing": ([vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64)], C.c_int),
         "rt_comm_deal_info": ([vp, C.POINTER(C.c_int), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                C.POINTER(C.c_uint64)], C.c_int),
+        "rt_comm_deal_hash": ([vp, C.POINTER(C.c_uint64)], C.c_int),
         "rt_camera_default": ([u32, u32, C.POINTER(Camera)], C.c_int),
         "rt_renderer_create": ([vp, u32, u32, C.POINTER(vp)], C.c_int),
         "rt_renderer_destroy": ([vp], C.c_int),

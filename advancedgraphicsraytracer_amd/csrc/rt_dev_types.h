@@ -156,8 +156,9 @@ struct TraceArgs {
 RT_DECLARE_LAUNCHERS(kcore)
 RT_DECLARE_LAUNCHERS(kext)
 #undef RT_DECLARE_LAUNCHERS
-// where: per global tile (shard << 24 | local tile) of an explicit deal; nullptr = interleaved
+// where: per global tile (shard << 24 | local tile) of an explicit deal; nullptr = interleaved.
+// first = 1: `gathered` holds shards 1.. only (rank 0's own tiles are already in `out`)
 void launch_assemble(const uint32_t *gathered, uint32_t cap, uint32_t nshards, const uint32_t *where, uint32_t tiles_x,
-                     uint32_t ntiles, uint32_t W, uint32_t H, uint32_t *out, hipStream_t st);
+                     uint32_t ntiles, uint32_t W, uint32_t H, uint32_t *out, hipStream_t st, uint32_t first = 0);
 
 }  // namespace rt

@@ -92,10 +92,19 @@ struct rt_scene {
     hipStream_t stream = nullptr;
 };
 
-// frames in flight of overlapped primary+shadow frames: up to 6 renderer streams (with the
-// caller's and a communicator's stream, 8 = the bench's GPU_MAX_HW_QUEUES)
+// renderer streams: up to 8 -- frames in flight of overlapped primary+shadow frames (timed
+// choice among 2 / 4 / 6, forced up to 8) and the path-state slots of pipelined path-traced
+// frames (8 for small batches when the process has >= 8 hardware queues, else 4).  With the
+// caller's stream and a communicator's a process may then drive 10 streams; HIP maps them onto
+// GPU_MAX_HW_QUEUES hardware queues (default 4, bench.py sets 8 for the workloads that overlap).
 constexpr int kPsMaxDepth = 8;   // renderer streams (frames in flight when forced: RT_PS_DEPTH)
 constexpr int kPtMaxSlots = 8;    // path-state slots of pipelined path-traced frames (RT_PT_SLOTS; <= kPsMaxDepth streams)
+// the process's hardware queues per device as HIP will use them (GPU_MAX_HW_QUEUES, default 4)
+inline int hw_queues() {
+    const char *e = std::getenv("GPU_MAX_HW_QUEUES");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 4;
+}
 
 struct rt_renderer {
     rt_scene *scene = nullptr;
@@ -658,12 +667,14 @@ uint64_t fnv1a(const void *d, size_t n, uint64_t h = 1469598103934665603ull) {
 }
 
 // an explicit deal's tile list on the device (FrameArgs::tile_map); a changed list waits for
-// every frame still reading the old one
-// key != 0: the caller's identity of the list (rt_multi.cpp's deals), used instead of its hash
-int set_tile_map(rt_renderer *r, const uint32_t *tiles, uint32_t n, uint32_t ntiles, uint64_t key = 0) {
-    const uint64_t h = key ? (key * 0x9e3779b97f4a7c15ull) ^ 0x5bd1e9955bd1e995ull
-                           : fnv1a(tiles, sizeof(uint32_t) * n, fnv1a(&n, sizeof(n)));
-    if (r->d_map && h == r->map_hash && r->map_host.size() == n) return RT_OK;
+// every frame still reading the old one.  The list in use is compared element by element (a
+// memcmp of at most ntiles words, the same O(n) as hashing it): a caller-supplied identity of
+// the list could repeat after its owner was freed and reallocated, and the range /
+// duplicate checks below must see every list that differs.
+int set_tile_map(rt_renderer *r, const uint32_t *tiles, uint32_t n, uint32_t ntiles) {
+    if (r->d_map && r->map_host.size() == n && (n == 0 || std::memcmp(r->map_host.data(), tiles, sizeof(uint32_t) * n) == 0))
+        return RT_OK;
+    const uint64_t h = fnv1a(tiles, sizeof(uint32_t) * n, fnv1a(&n, sizeof(n)));
     std::vector<uint8_t> seen(ntiles, 0);
     for (uint32_t i = 0; i < n; ++i) {
         if (tiles[i] >= ntiles || seen[tiles[i]]) return fail(RT_ERR_INVALID, "tile list: index out of range or repeated");
@@ -785,7 +796,11 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
             // its deep paths' latency chain, and 8 frames in flight overlap more of it (1/8 shard
             // 1.24 -> 1.16-1.18 ms); whole 1080p x 16 spp frames lose with more than 4 (7.51 ->
             // 7.61 / 7.72 ms with 6 / 8; profiles/r04/slots)
-            uint32_t k = s->pt_slots ? s->pt_slots : (np <= (8400u << 10) ? 8u : 4u);
+            // (measured with GPU_MAX_HW_QUEUES=8, as bench.py runs path-traced and multi-GPU
+            // workloads; with HIP's default of 4 queues eight slot streams share them and the
+            // measurement does not carry over, so the small-batch default is 8 only when the
+            // process has at least 8 hardware queues -- ADVICE r4)
+            uint32_t k = s->pt_slots ? s->pt_slots : (np <= (8400u << 10) && hw_queues() >= 8 ? 8u : 4u);
             while (k > 2 && (double)k * need + (8ull << 30) > avail) --k;
             for (uint32_t j = k; j < (uint32_t)kPtMaxSlots; ++j) {
                 if (r->d_pt[j]) HIP_TRY(hipFree(r->d_pt[j]));
@@ -1125,8 +1140,7 @@ int tune_gate(rt_renderer *r, uint64_t key, hipStream_t st, bool &open) {
 }
 
 int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
-                  uint32_t *out, int packed, void *stream, const uint32_t *tiles = nullptr, uint32_t ntiles_map = 0,
-                  uint64_t tiles_key = 0) {
+                  uint32_t *out, int packed, void *stream, const uint32_t *tiles = nullptr, uint32_t ntiles_map = 0) {
     if (!r || !cam || !p || !out) return fail(RT_ERR_INVALID, "rt_render: null argument");
     if (p->width != r->W || p->height != r->H)
         return fail(RT_ERR_INVALID, "frame size differs from the renderer's accumulator");
@@ -1148,7 +1162,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     F.shard = shard; F.nshards = nshards; F.tiles_x = tiles_x;
     F.ntiles_local = shard < ntiles ? (ntiles - shard + nshards - 1) / nshards : 0;
     if (tiles) {   // an explicit deal (rt_render_shard_tiles)
-        int rc = set_tile_map(r, tiles, ntiles_map, ntiles, tiles_key);
+        int rc = set_tile_map(r, tiles, ntiles_map, ntiles);
         if (rc != RT_OK) return rc;
         F.ntiles_local = ntiles_map;
         F.tile_map = r->d_map;
@@ -1493,10 +1507,11 @@ int rt::accumulator_unpack(rt_renderer *r, const uint32_t *tiles_dev, uint32_t n
     return acc_tiles(r, tiles_dev, n, const_cast<void *>(buf_dev), stream, 1);
 }
 
-int rt::render_shard_tiles_keyed(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, const uint32_t *tiles,
-                                 uint32_t n, uint64_t key, uint32_t *out_dev, void *stream) {
-    if (!r || (n && !tiles)) return fail(RT_ERR_INVALID, "render_shard_tiles_keyed: null argument");
-    return launch_render(r, cam, p, 0, 1, out_dev, 1, stream, tiles ? tiles : reinterpret_cast<const uint32_t *>(r), n, key);
+int rt::render_part(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
+                    const uint32_t *tiles, uint32_t n, int packed, uint32_t *out_dev, void *stream) {
+    if (!r) return fail(RT_ERR_INVALID, "render_part: null renderer");
+    if (tiles || n) return launch_render(r, cam, p, 0, 1, out_dev, packed, stream, tiles ? tiles : reinterpret_cast<const uint32_t *>(r), n);
+    return launch_render(r, cam, p, shard, nshards, out_dev, packed, stream);
 }
 
 int rt::renderer_geometry(const rt_renderer *r, uint32_t *W, uint32_t *H, int *device) {

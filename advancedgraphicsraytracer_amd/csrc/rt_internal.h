@@ -53,10 +53,12 @@ int renderer_geometry(const rt_renderer *r, uint32_t *W, uint32_t *H, int *devic
 int renderer_accumulator(rt_renderer *r, void **acc_dev, size_t *bytes);
 int accumulator_pack(rt_renderer *r, const uint32_t *tiles_dev, uint32_t n, void *buf_dev, void *stream);
 int accumulator_unpack(rt_renderer *r, const uint32_t *tiles_dev, uint32_t n, const void *buf_dev, void *stream);
-// rt_render_shard_tiles with the caller's identity of the tile list (key != 0): the multi-GPU
-// frame renders the same deal frame after frame and the renderer then skips hashing the list
-int render_shard_tiles_keyed(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, const uint32_t *tiles,
-                             uint32_t n, uint64_t key, uint32_t *out_dev, void *stream);
+// one rank's part of a multi-GPU frame (rt_multi.cpp): the interleaved shard `shard` of
+// `nshards`, or the explicit tile list `tiles` (n tiles; n == 0 with tiles != NULL: none),
+// written packed ([local tile][64], rt_render_shard's layout) or, packed == 0, straight into a
+// row-major W x H frame at the tiles' own pixels (rank 0 renders its tiles into the output frame)
+int render_part(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
+                const uint32_t *tiles, uint32_t n, int packed, uint32_t *out_dev, void *stream);
 
 // SURVEY.md 8(d) scenes as descriptions
 struct SceneSource {

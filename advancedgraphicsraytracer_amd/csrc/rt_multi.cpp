@@ -13,6 +13,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -108,12 +110,15 @@ int comm_fail(const Rccl &R, ncclResult_t e, const char *what) {
 
 // A deal: which rank renders which 8x8 tiles (the rt_tile_deal layout: rank k owns
 // tiles[off[k] .. off[k+1])).  The interleaved deal t % world == rank has id 0; cost-balanced
-// deals (RT_MULTI_BALANCED) get ids 1, 2, ... in the order they are built.  Rank 0 keeps a
-// device map for the assembly of a balanced deal: (shard << 24 | local index) per global tile.
+// deals (RT_MULTI_BALANCED) take ids from one process-wide counter, so an id never repeats --
+// not even for a communicator allocated where a destroyed one lived.  Rank 0 keeps a device map
+// for the assembly of a balanced deal: (shard << 24 | local index) per global tile.  `hash`
+// (FNV-1a of tiles and offsets) is the same on every rank and in every run that builds the
+// same deal (rt_comm_deal_hash).
 struct Deal {
     std::vector<uint32_t> tiles, off;
     std::vector<uint8_t> owner;            // rank of every global tile
-    uint64_t id = 0;
+    uint64_t id = 0, hash = 0;
     uint32_t *d_where = nullptr;
     int device = 0;
     uint32_t count(int k) const { return off[k + 1] - off[k]; }
@@ -130,6 +135,10 @@ using DealP = std::shared_ptr<const Deal>;
 // Every collective after set-up -- the per-frame gathers, the cost exchange and the accumulator
 // moves of a deal change -- runs on the communicator's own stream, so the communicator's
 // operations are serialised in issue order on every rank whatever streams the caller uses.
+// Rank 0 renders its own tiles straight into a row-major frame (the caller's in flags-0 mode,
+// its own frame[k] when pipelined): the gather brings only the peers' packed tiles and the
+// assembly scatters only those (round 5; at world 1 there is no gather, no assembly and no
+// cross-stream event at all).
 struct rt_comm {
     ncclComm_t comm = nullptr;
     bool owned = false;
@@ -138,19 +147,22 @@ struct rt_comm {
     const rt_renderer *renderer = nullptr; // buffers below belong to this renderer's frame size
     uint32_t W = 0, H = 0, ntiles = 0;
     uint32_t stride = 0;                   // packed pixels per shard slot (room for any deal)
-    uint32_t *tiles[2] = {nullptr, nullptr};      // this rank's packed tiles (rank 0: unused)
-    uint32_t *gathered[2] = {nullptr, nullptr};   // rank 0: world x stride, slot 0 rendered in place
-    hipEvent_t ev_render[2] = {nullptr, nullptr}, ev_gather[2] = {nullptr, nullptr};
-    hipEvent_t ev_asm[2] = {nullptr, nullptr};   // rank 0, pipelined: frame assembled (comm stream)
-    hipEvent_t ev_caller = nullptr;        // rank 0, pipelined: the caller's stream at the call, so the
-                                           // unshuffle into rgb8_dev follows the caller's reads of it
+    uint32_t *tiles[2] = {nullptr, nullptr};      // rank > 0: this rank's packed tiles
+    uint32_t *gathered[2] = {nullptr, nullptr};   // rank 0: (world - 1) x stride, peer p at (p - 1) x stride
+    uint32_t *frame[2] = {nullptr, nullptr};      // rank 0, pipelined: slot k's row-major frame
+    hipEvent_t ev_render[2] = {nullptr, nullptr}; // rank > 0: render done (caller's stream)
+    hipEvent_t ev_gather[2] = {nullptr, nullptr}; // gather / send done (communicator's stream)
+    hipEvent_t ev_asm[2] = {nullptr, nullptr};    // rank 0, pipelined: peers' tiles scattered into frame[k]
+    hipEvent_t ev_copy[2] = {nullptr, nullptr};   // rank 0, pipelined: frame[k] copied out (caller's stream)
+    bool sent[2] = {false, false}, copied[2] = {false, false};   // ev_gather / ev_copy recorded
+    hipEvent_t ev_caller = nullptr;        // rank 0, flags 0: the caller's stream at the call
     hipEvent_t ev_mig[2] = {nullptr, nullptr};   // accumulator move: caller -> comm stream -> caller
     int slot = 0;
     int pending = -1;                      // slot whose gather is in flight (pipelined mode)
     DealP slot_deal[2];                    // the deal a slot's frame was rendered under
     uint64_t frames = 0;
     DealP interleaved, cur;                // cur: the deal frames are rendered under now
-    uint64_t deals_built = 0;              // balanced deals built (their ids)
+    uint64_t deals_built = 0;              // balanced deals built by this communicator
     // RT_MULTI_BALANCED: a parameter set (camera, size, spp, depth, mode) tries to balance the
     // deal on its kDealAfter-th frame, then after 2x, 4x, ... as many frames until every rank has
     // measured tile costs (a renderer records them once its own timed choices are done), and not
@@ -163,6 +175,8 @@ struct rt_comm {
     void *d_mig_send = nullptr, *d_mig_recv = nullptr;   // accumulator moves: ntiles x 64 float4 each
     uint32_t *d_mig_list = nullptr;        // ... their tile lists (2 x ntiles)
     uint32_t *h_mig_list = nullptr;        // pinned host staging of those lists
+    uint32_t *d_status = nullptr;          // accumulator moves: world status words (own at [rank])
+    uint32_t *h_status = nullptr;          // ... read back (pinned)
     bool mig_pending = false;              // ev_mig[1] marks a move whose list upload may still run
     uint64_t n_exchanges = 0, n_migrations = 0, n_mig_skipped = 0;
     // RT_MULTI_TIMING: per frame (render start, render end, gather end) events, summed by rt_comm_timing
@@ -176,19 +190,36 @@ namespace {
 // its tile costs within its first frames unless a timed camera walk holds them back
 constexpr uint32_t kDealAfter = 6;
 
+// balanced deal ids: one counter for the process (never reused, see Deal)
+std::atomic<uint64_t> g_deal_serial{0};
+
+// Test-only fault injection (RT_MULTI_FAULT=<site>:<rank>): the named local step fails on that
+// rank, so the tests can check that every rank of a per-frame collective returns an error and
+// none is left waiting in it.  Sites: cost_upload (rebalance's block upload), mig_pack
+// (migrate's accumulator_pack).  Unset in production.
+bool injected(const rt_comm *c, const char *site) {
+    const char *e = std::getenv("RT_MULTI_FAULT");
+    if (!e) return false;
+    const size_t n = std::strlen(site);
+    return std::strncmp(e, site, n) == 0 && e[n] == ':' && std::atoi(e + n + 1) == c->rank;
+}
+
 void free_buffers(rt_comm *c) {
     for (int k = 0; k < 2; ++k) {
-        if (c->tiles[k]) (void)hipFree(c->tiles[k]);
-        if (c->gathered[k]) (void)hipFree(c->gathered[k]);
-        c->tiles[k] = c->gathered[k] = nullptr;
+        for (uint32_t **q : {&c->tiles[k], &c->gathered[k], &c->frame[k]}) {
+            if (*q) (void)hipFree(*q);
+            *q = nullptr;
+        }
         c->slot_deal[k].reset();
+        c->sent[k] = c->copied[k] = false;
     }
-    for (void *p : {(void *)c->d_setup, c->d_mig_send, c->d_mig_recv, (void *)c->d_mig_list})
+    for (void *p : {(void *)c->d_setup, c->d_mig_send, c->d_mig_recv, (void *)c->d_mig_list, (void *)c->d_status})
         if (p) (void)hipFree(p);
-    if (c->h_mig_list) (void)hipHostFree(c->h_mig_list);
-    c->h_mig_list = nullptr;
+    for (void *p : {(void *)c->h_mig_list, (void *)c->h_status})
+        if (p) (void)hipHostFree(p);
+    c->h_mig_list = c->h_status = nullptr;
     c->mig_pending = false;
-    c->d_setup = c->d_mig_list = nullptr;
+    c->d_setup = c->d_mig_list = c->d_status = nullptr;
     c->d_mig_send = c->d_mig_recv = nullptr;
     c->interleaved.reset();
     c->cur.reset();
@@ -200,12 +231,24 @@ void free_buffers(rt_comm *c) {
     c->settled = false;
 }
 
+uint64_t deal_hash(const std::vector<uint32_t> &tiles, const std::vector<uint32_t> &off) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const std::vector<uint32_t> &v) {
+        for (uint32_t x : v)
+            for (int b = 0; b < 4; ++b) h = (h ^ ((x >> (8 * b)) & 0xffu)) * 1099511628211ull;
+    };
+    mix(tiles);
+    mix(off);
+    return h;
+}
+
 // a deal from its tile lists; rank 0 uploads the assembly map of a balanced one
 int make_deal(rt_comm *c, std::vector<uint32_t> tiles, std::vector<uint32_t> off, uint64_t id, DealP &out) {
     auto d = std::make_shared<Deal>();
     d->tiles = std::move(tiles);
     d->off = std::move(off);
     d->id = id;
+    d->hash = deal_hash(d->tiles, d->off);
     d->device = c->device;
     d->owner.assign(c->ntiles, 0);
     std::vector<uint32_t> where(c->ntiles, 0);
@@ -214,7 +257,7 @@ int make_deal(rt_comm *c, std::vector<uint32_t> tiles, std::vector<uint32_t> off
             d->owner[d->tiles[i]] = (uint8_t)k;
             where[d->tiles[i]] = ((uint32_t)k << 24) | (i - d->off[k]);
         }
-    if (c->rank == 0 && id != 0) {
+    if (c->rank == 0 && id != 0 && c->world > 1) {
         HIP_TRY(hipMalloc(&d->d_where, sizeof(uint32_t) * c->ntiles));
         HIP_TRY(hipMemcpy(d->d_where, where.data(), sizeof(uint32_t) * c->ntiles, hipMemcpyHostToDevice));
     }
@@ -235,8 +278,12 @@ int bind_renderer(rt_comm *c, rt_renderer *r) {
     // every deal fits: a shard holds at most all tiles (a balanced deal's region may hold many cheap ones)
     const uint32_t stride = ntiles * 64u;
     for (int k = 0; k < 2; ++k) {
-        if (c->rank == 0) HIP_TRY(hipMalloc(&c->gathered[k], sizeof(uint32_t) * (size_t)stride * c->world));
-        else HIP_TRY(hipMalloc(&c->tiles[k], sizeof(uint32_t) * (size_t)stride));
+        if (c->rank == 0) {
+            HIP_TRY(hipMalloc(&c->frame[k], sizeof(uint32_t) * (size_t)W * H));
+            if (c->world > 1) HIP_TRY(hipMalloc(&c->gathered[k], sizeof(uint32_t) * (size_t)stride * (c->world - 1)));
+        } else {
+            HIP_TRY(hipMalloc(&c->tiles[k], sizeof(uint32_t) * (size_t)stride));
+        }
     }
     if (c->world > 1) {
         HIP_TRY(hipMalloc(&c->d_setup, sizeof(uint32_t) * ((size_t)ntiles + 2) * c->world));
@@ -244,6 +291,8 @@ int bind_renderer(rt_comm *c, rt_renderer *r) {
         HIP_TRY(hipMalloc(&c->d_mig_recv, (size_t)stride * 16u));
         HIP_TRY(hipMalloc(&c->d_mig_list, sizeof(uint32_t) * 2u * ntiles));
         HIP_TRY(hipHostMalloc(&c->h_mig_list, sizeof(uint32_t) * 2u * ntiles, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(&c->d_status, sizeof(uint32_t) * (size_t)c->world));
+        HIP_TRY(hipHostMalloc(&c->h_status, sizeof(uint32_t) * (size_t)c->world, hipHostMallocDefault));
     }
     c->W = W;
     c->H = H;
@@ -261,15 +310,15 @@ int bind_renderer(rt_comm *c, rt_renderer *r) {
     return RT_OK;
 }
 
-// the frame's one collective: every rank's packed tiles to rank 0 (rank 0's own shard was
-// rendered in place into slot 0 of the gather buffer); each peer sends its deal's tile count
+// the frame's one collective: every peer's packed tiles to rank 0 (rank 0's own tiles are in
+// its frame already); each peer sends its deal's tile count
 int gather(rt_comm *c, int k, const Deal &d, hipStream_t st) {
     const Rccl &R = rccl();
     NCCL_TRY(R, R.group_start(), "ncclGroupStart");
     if (c->rank == 0) {
         for (int peer = 1; peer < c->world; ++peer) {
             const size_t bytes = sizeof(uint32_t) * 64u * d.count(peer);
-            ncclResult_t e = R.recv(c->gathered[k] + (size_t)peer * c->stride, bytes, ncclUint8, peer, c->comm, st);
+            ncclResult_t e = R.recv(c->gathered[k] + (size_t)(peer - 1) * c->stride, bytes, ncclUint8, peer, c->comm, st);
             if (e != ncclSuccess) {
                 (void)R.group_end();
                 return comm_fail(R, e, "ncclRecv");
@@ -296,13 +345,12 @@ unsigned sync_event_flags() {
     return hipEventDisableTiming | (e && std::strcmp(e, "system") == 0 ? 0u : (unsigned)hipEventReleaseToDevice);
 }
 
-// rank 0: slot k's gathered shards -> the row-major frame, under the deal that slot was rendered with
-int assemble(rt_comm *c, int k, uint32_t *rgb8, hipStream_t st) {
-    if (c->rank != 0) return RT_OK;
-    if (!rgb8) return fail(RT_ERR_INVALID, "rt_render_frame_multi: rank 0 needs an output frame");
+// rank 0: slot k's gathered peer tiles -> their pixels of the row-major frame `out`, under the
+// deal that slot was rendered with (rank 0's own tiles are already there)
+int scatter_peers(rt_comm *c, int k, uint32_t *out, hipStream_t st) {
     const Deal &d = *c->slot_deal[k];
     launch_assemble(c->gathered[k], c->stride, (uint32_t)c->world, d.id ? d.d_where : nullptr, (c->W + 7) / 8,
-                    c->ntiles, c->W, c->H, rgb8, st);
+                    c->ntiles, c->W, c->H, out, st, 1u);
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }
@@ -319,12 +367,18 @@ uint64_t params_key(const rt_camera *cam, const rt_frame_params *p) {
     return h;
 }
 
+// The exchanged tile costs (wave cycles) move by a few percent between runs of the same frame;
+// the deal is cut on costs rounded to 1/kCostQuant of the frame's mean tile cost, so that such
+// noise rarely moves a cut (rt_comm_deal_hash reports the deal actually built).
+constexpr double kCostQuant = 64.0;
+
 // One balancing attempt (every rank, the same call): an all-gather of the ranks' measured tile
 // costs under the current deal -- each rank sends one block [status, count, costs] to every
 // peer inside one group -- then every rank builds the same rt_tile_deal over the whole frame
 // (deterministic host code on identical inputs).  The status words make the outcome collective:
-// a rank that could not read its costs fails the call on every rank, and the deal changes only
-// when every rank measured its tiles (`complete`).  Blocking: O(log frames) calls per parameter set.
+// a rank that could not read its costs, or could not upload its block, still enters the group
+// (its status word says so) and the call then fails on every rank; the deal changes only when
+// every rank measured its tiles (`complete`).  Blocking: O(log frames) calls per parameter set.
 int rebalance(rt_comm *c, rt_renderer *r, DealP &next, bool &complete) {
     const Rccl &R = rccl();
     const Deal &cur = *c->cur;
@@ -341,7 +395,13 @@ int rebalance(rt_comm *c, rt_renderer *r, DealP &next, bool &complete) {
     block[1] = mine;
     hipStream_t st = c->comm_stream;
     uint32_t *own = c->d_setup + (size_t)c->rank * B;
-    HIP_TRY(hipMemcpyAsync(own, block.data(), sizeof(uint32_t) * B, hipMemcpyHostToDevice, st));
+    int local = lrc;
+    hipError_t up = injected(c, "cost_upload") ? hipErrorInvalidValue
+                                               : hipMemcpyAsync(own, block.data(), sizeof(uint32_t) * B, hipMemcpyHostToDevice, st);
+    if (up != hipSuccess) {   // the peers learn it from the status word; the group runs anyway
+        local = fail(RT_ERR_HIP, std::string("cost upload: ") + hipGetErrorString(up));
+        (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(own), 2u, 1, st);
+    }
     NCCL_TRY(R, R.group_start(), "ncclGroupStart");
     for (int q = 0; q < c->world; ++q) {
         if (q == c->rank) continue;
@@ -357,24 +417,31 @@ int rebalance(rt_comm *c, rt_renderer *r, DealP &next, bool &complete) {
     HIP_TRY(hipMemcpyAsync(all.data(), c->d_setup, sizeof(uint32_t) * all.size(), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     c->n_exchanges += 1;
-    if (lrc != RT_OK) return lrc;
+    if (local != RT_OK) return local;
     complete = true;
     for (int k = 0; k < c->world; ++k) {
         const uint32_t status = all[(size_t)k * B];
-        if (status & 2u) return fail(RT_ERR_COMM, "rt_render_frame_multi: rank " + std::to_string(k) + " could not read its tile costs");
+        if (status & 2u) return fail(RT_ERR_COMM, "rt_render_frame_multi: rank " + std::to_string(k) + " failed before the cost exchange");
         if (all[(size_t)k * B + 1] != cur.count(k)) return fail(RT_ERR_COMM, "rt_render_frame_multi: ranks disagree on the deal");
         complete = complete && (status & 1u);
     }
     next = c->cur;
     if (!complete) return RT_OK;   // e.g. a renderer still timing its camera walk: try again later
     std::vector<uint32_t> global(c->ntiles, 0u);
+    double total = 0.0;
     for (int k = 0; k < c->world; ++k)
-        for (uint32_t i = 0; i < cur.count(k); ++i) global[cur.tiles[cur.off[k] + i]] = all[(size_t)k * B + 2 + i];
+        for (uint32_t i = 0; i < cur.count(k); ++i) {
+            global[cur.tiles[cur.off[k] + i]] = all[(size_t)k * B + 2 + i];
+            total += all[(size_t)k * B + 2 + i];
+        }
+    const double q = std::max(1.0, total / c->ntiles / kCostQuant);
+    for (uint32_t &x : global) x = (uint32_t)std::min(4294967295.0, std::floor(x / q + 0.5));
     std::vector<uint32_t> tiles(c->ntiles), off((size_t)c->world + 1);
     int rc = rt_tile_deal(c->W, c->H, global.data(), (uint32_t)c->world, tiles.data(), off.data());
     if (rc != RT_OK) return rc;
     if (tiles == cur.tiles && off == cur.off) return RT_OK;
-    return make_deal(c, std::move(tiles), std::move(off), ++c->deals_built, next);
+    c->deals_built += 1;
+    return make_deal(c, std::move(tiles), std::move(off), ++g_deal_serial, next);
 }
 
 // Tiles change owner between two frames: a pixel's running average (renderer.cpp:235-241) must
@@ -383,7 +450,11 @@ int rebalance(rt_comm *c, rt_renderer *r, DealP &next, bool &complete) {
 // `to` (one group of point-to-point transfers, each pair's tiles in `from` order) and writes the
 // ones it receives into its accumulator.  In stream order: the caller's stream's earlier frames
 // have updated the accumulator before the pack, and its next frame renders after the unpack --
-// no host synchronisation, no whole-frame broadcast.  Frames that reset the accumulator skip it.
+// no whole-frame broadcast.  Frames that reset the accumulator skip it.
+// Failure is collective: a rank whose local steps (the staging wait, the list upload, the pack)
+// fail still enters the group, and every rank's status word travels with the data; the ranks
+// read the statuses back (one host synchronisation per deal change) and unpack only when all
+// are clean -- otherwise every rank returns RT_ERR_COMM, keeps the old deal and its accumulator.
 int migrate(rt_comm *c, rt_renderer *r, const Deal &from, const Deal &to, hipStream_t st) {
     const Rccl &R = rccl();
     std::vector<uint32_t> L;
@@ -401,13 +472,24 @@ int migrate(rt_comm *c, rt_renderer *r, const Deal &from, const Deal &to, hipStr
     }
     const uint32_t nrecv = (uint32_t)L.size() - nsend;
     hipStream_t cs = c->comm_stream;
-    HIP_TRY(hipEventRecord(c->ev_mig[0], st));
-    HIP_TRY(hipStreamWaitEvent(cs, c->ev_mig[0], 0));
-    if (c->mig_pending) HIP_TRY(hipEventSynchronize(c->ev_mig[1]));   // the previous move read the staging
-    std::copy(L.begin(), L.end(), c->h_mig_list);
-    if (!L.empty()) HIP_TRY(hipMemcpyAsync(c->d_mig_list, c->h_mig_list, sizeof(uint32_t) * L.size(), hipMemcpyHostToDevice, cs));
-    int rc = accumulator_pack(r, c->d_mig_list, nsend, c->d_mig_send, cs);
-    if (rc != RT_OK) return rc;
+    int local = RT_OK;
+    auto step = [&](hipError_t e, const char *what) {
+        if (local == RT_OK && e != hipSuccess) local = fail(RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    };
+    step(hipEventRecord(c->ev_mig[0], st), "hipEventRecord");
+    step(hipStreamWaitEvent(cs, c->ev_mig[0], 0), "hipStreamWaitEvent");
+    if (local == RT_OK && c->mig_pending) step(hipEventSynchronize(c->ev_mig[1]), "staging wait");   // the previous move read it
+    if (local == RT_OK) {
+        std::copy(L.begin(), L.end(), c->h_mig_list);
+        if (!L.empty())
+            step(hipMemcpyAsync(c->d_mig_list, c->h_mig_list, sizeof(uint32_t) * L.size(), hipMemcpyHostToDevice, cs), "move list upload");
+    }
+    if (local == RT_OK) {
+        local = injected(c, "mig_pack") ? fail(RT_ERR_HIP, "accumulator_pack: injected fault (RT_MULTI_FAULT)")
+                                        : accumulator_pack(r, c->d_mig_list, nsend, c->d_mig_send, cs);
+    }
+    // this rank's status word (a memset on the stream, so it follows whatever ran before)
+    (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->d_status + c->rank), local == RT_OK ? 0u : 1u, 1, cs);
     const size_t tile_bytes = 64u * 16u;
     char *sb = static_cast<char *>(c->d_mig_send), *rb = static_cast<char *>(c->d_mig_recv);
     NCCL_TRY(R, R.group_start(), "ncclGroupStart");
@@ -418,13 +500,23 @@ int migrate(rt_comm *c, rt_renderer *r, const Deal &from, const Deal &to, hipStr
             e = R.send(sb + send_off[q] * tile_bytes, (send_off[q + 1] - send_off[q]) * tile_bytes, ncclUint8, q, c->comm, cs);
         if (e == ncclSuccess && recv_off[q + 1] > recv_off[q])
             e = R.recv(rb + recv_off[q] * tile_bytes, (recv_off[q + 1] - recv_off[q]) * tile_bytes, ncclUint8, q, c->comm, cs);
+        if (e == ncclSuccess) e = R.send(c->d_status + c->rank, sizeof(uint32_t), ncclUint8, q, c->comm, cs);
+        if (e == ncclSuccess) e = R.recv(c->d_status + q, sizeof(uint32_t), ncclUint8, q, c->comm, cs);
         if (e != ncclSuccess) {
             (void)R.group_end();
             return comm_fail(R, e, "accumulator move");
         }
     }
     NCCL_TRY(R, R.group_end(), "ncclGroupEnd");
-    if ((rc = accumulator_unpack(r, c->d_mig_list + nsend, nrecv, c->d_mig_recv, cs)) != RT_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(c->h_status, c->d_status, sizeof(uint32_t) * c->world, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
+    c->mig_pending = false;   // the stream is drained: the staging is free again
+    if (local != RT_OK) return local;
+    for (int q = 0; q < c->world; ++q)
+        if (c->h_status[q] != 0u)
+            return fail(RT_ERR_COMM, "rt_render_frame_multi: rank " + std::to_string(q) + " failed its part of the accumulator move");
+    int rc = accumulator_unpack(r, c->d_mig_list + nsend, nrecv, c->d_mig_recv, cs);
+    if (rc != RT_OK) return rc;
     HIP_TRY(hipEventRecord(c->ev_mig[1], cs));
     HIP_TRY(hipStreamWaitEvent(st, c->ev_mig[1], 0));
     c->mig_pending = true;
@@ -537,12 +629,9 @@ int rt_comm_destroy(rt_comm *c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     free_buffers(c);
-    for (int k = 0; k < 2; ++k) {
-        if (c->ev_render[k]) (void)hipEventDestroy(c->ev_render[k]);
-        if (c->ev_gather[k]) (void)hipEventDestroy(c->ev_gather[k]);
-        if (c->ev_asm[k]) (void)hipEventDestroy(c->ev_asm[k]);
-        if (c->ev_mig[k]) (void)hipEventDestroy(c->ev_mig[k]);
-    }
+    for (int k = 0; k < 2; ++k)
+        for (hipEvent_t e : {c->ev_render[k], c->ev_gather[k], c->ev_asm[k], c->ev_copy[k], c->ev_mig[k]})
+            if (e) (void)hipEventDestroy(e);
     if (c->ev_caller) (void)hipEventDestroy(c->ev_caller);
     for (auto &e : c->tev)
         for (auto &x : e) (void)hipEventDestroy(x);
@@ -568,6 +657,12 @@ int rt_comm_deal_info(const rt_comm *c, int *balanced, uint32_t *ntiles, uint32_
     return RT_OK;
 }
 
+int rt_comm_deal_hash(const rt_comm *c, uint64_t *hash) {
+    if (!c || !hash) return fail(RT_ERR_INVALID, "rt_comm_deal_hash: null argument");
+    *hash = c->cur ? c->cur->hash : 0u;
+    return RT_OK;
+}
+
 int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, const rt_frame_params *p,
                           uint32_t *rgb8_dev, uint32_t flags, void *stream) {
     if (!r || !c || !cam || !p) return fail(RT_ERR_INVALID, "rt_render_frame_multi: null argument");
@@ -580,25 +675,23 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
         return fail(RT_ERR_INVALID, "rt_render_frame_multi: a pipelined frame is pending (rt_multi_flush)");
     if (c->rank == 0 && !rgb8_dev && (!pipelined || c->pending >= 0))
         return fail(RT_ERR_INVALID, "rt_render_frame_multi: rank 0 needs an output frame");
+    {
+        uint32_t W = 0, H = 0;
+        int dev = 0;
+        if (renderer_geometry(r, &W, &H, &dev) == RT_OK && (p->width != W || p->height != H))
+            return fail(RT_ERR_INVALID, "frame size differs from the renderer's accumulator");
+    }
     HIP_TRY(hipSetDevice(c->device));
     if (!c->comm_stream) {
         HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
-        for (int j = 0; j < 2; ++j) {
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_render[j], sync_event_flags()));
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_gather[j], sync_event_flags()));
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_asm[j], sync_event_flags()));
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_mig[j], sync_event_flags()));
-        }
+        for (int j = 0; j < 2; ++j)
+            for (hipEvent_t *e : {&c->ev_render[j], &c->ev_gather[j], &c->ev_asm[j], &c->ev_copy[j], &c->ev_mig[j]})
+                HIP_TRY(hipEventCreateWithFlags(e, sync_event_flags()));
         HIP_TRY(hipEventCreateWithFlags(&c->ev_caller, sync_event_flags()));
     }
     int rc = bind_renderer(c, r);
     if (rc != RT_OK) return rc;
     hipStream_t st = (hipStream_t)stream;
-    // rank 0, pipelined: this call unshuffles the previous frame into rgb8_dev on the
-    // communicator's stream; whatever the caller queued on its stream before this call (a copy
-    // or display of the frame before) must be done with rgb8_dev first
-    const bool assemble_prev = pipelined && c->rank == 0 && c->pending >= 0;
-    if (assemble_prev) HIP_TRY(hipEventRecord(c->ev_caller, st));
     // the deal of this frame: the interleaved one, or with RT_MULTI_BALANCED the last deal
     // balanced on measured tile costs -- kept across camera moves; each parameter set tries to
     // rebalance on its kDealAfter-th frame (then 2x, 4x, ... until every rank has costs).  Every
@@ -607,6 +700,9 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
     if (c->world > 1) {
         if (!(flags & RT_MULTI_BALANCED)) {
             next = c->interleaved;
+            // re-enabling the flag later starts the balancing schedule again
+            c->pkey = 0;
+            c->settled = false;
         } else {
             const uint64_t key = params_key(cam, p);
             if (key != c->pkey) {
@@ -633,8 +729,7 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
     }
     const Deal &deal = *c->cur;
     const int k = c->slot;
-    c->slot_deal[k] = c->cur;
-    uint32_t *mine = c->rank == 0 ? c->gathered[k] : c->tiles[k];
+    const bool peers = c->world > 1;
     std::array<hipEvent_t, 3> *tv = nullptr;
     if (flags & RT_MULTI_TIMING) {
         if (c->tev_used == c->tev.size()) {
@@ -643,51 +738,92 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
             c->tev.push_back(e);
         }
         tv = &c->tev[c->tev_used++];
-        HIP_TRY(hipEventRecord((*tv)[0], st));
     }
-    if (deal.id != 0) {
-        // the renderer keys its tile map by (communicator, deal, rank) instead of hashing the list
-        const uint64_t key = ((uint64_t)(uintptr_t)c * 0x100000001b3ull) ^ (deal.id << 8) ^ (uint64_t)c->rank;
-        rc = render_shard_tiles_keyed(r, cam, p, deal.tiles.data() + deal.off[c->rank], deal.count(c->rank), key | 1u,
-                                      mine, st);
-    } else {
-        rc = rt_render_shard(r, cam, p, (uint32_t)c->rank, (uint32_t)c->world, mine, st);
-    }
-    if (rc != RT_OK) return rc;
-    if (tv) HIP_TRY(hipEventRecord((*tv)[1], st));
-    if (!pipelined) {   // the gather on the communicator's stream after the render; the caller's
-                        // stream waits for it, then rank 0 assembles on it
+    auto render = [&](uint32_t *out, int packed) -> int {
+        if (tv) HIP_TRY(hipEventRecord((*tv)[0], st));
+        int e = deal.id != 0
+                    ? render_part(r, cam, p, 0, 1, deal.tiles.data() + deal.off[c->rank], deal.count(c->rank), packed, out, st)
+                    : render_part(r, cam, p, (uint32_t)c->rank, (uint32_t)c->world, nullptr, 0, packed, out, st);
+        if (e != RT_OK) return e;
+        if (tv) HIP_TRY(hipEventRecord((*tv)[1], st));
+        return RT_OK;
+    };
+
+    if (c->rank != 0) {
+        // peers: packed tiles into slot k, then the send on the communicator's stream.  The slot
+        // was last read by the send of two frames back (pipelined) -- wait for that one only.
+        if (c->sent[k]) HIP_TRY(hipStreamWaitEvent(st, c->ev_gather[k], 0));
+        c->slot_deal[k] = c->cur;
+        if ((rc = render(c->tiles[k], 1)) != RT_OK) return rc;
         HIP_TRY(hipEventRecord(c->ev_render[k], st));
         HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_render[k], 0));
         if ((rc = gather(c, k, deal, c->comm_stream)) != RT_OK) return rc;
         HIP_TRY(hipEventRecord(c->ev_gather[k], c->comm_stream));
-        HIP_TRY(hipStreamWaitEvent(st, c->ev_gather[k], 0));
-        if (tv) HIP_TRY(hipEventRecord((*tv)[2], st));
-        if ((rc = assemble(c, k, rgb8_dev, st)) != RT_OK) return rc;
+        c->sent[k] = true;
+        if (tv) HIP_TRY(hipEventRecord((*tv)[2], c->comm_stream));
+        if (!pipelined) {   // in stream order: the call's work includes the send
+            HIP_TRY(hipStreamWaitEvent(st, c->ev_gather[k], 0));
+            c->frames += 1;
+            return RT_OK;
+        }
+        if (c->pending >= 0) c->frames += 1;
+        c->pending = k;
+        c->slot = k ^ 1;
+        return RT_OK;
+    }
+
+    if (!pipelined) {
+        // rank 0, flags 0: its tiles straight into rgb8_dev; the gather waits only for the caller's
+        // earlier work (the previous frame's scatter read gathered[k] on the caller's stream),
+        // and the peers' tiles are scattered on the caller's stream behind it
+        c->slot_deal[k] = c->cur;
+        if (peers) {
+            HIP_TRY(hipEventRecord(c->ev_caller, st));
+            HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_caller, 0));
+            if ((rc = gather(c, k, deal, c->comm_stream)) != RT_OK) return rc;
+            HIP_TRY(hipEventRecord(c->ev_gather[k], c->comm_stream));
+        }
+        if ((rc = render(rgb8_dev, 0)) != RT_OK) return rc;
+        if (peers) {
+            HIP_TRY(hipStreamWaitEvent(st, c->ev_gather[k], 0));
+            if (tv) HIP_TRY(hipEventRecord((*tv)[2], st));
+            if ((rc = scatter_peers(c, k, rgb8_dev, st)) != RT_OK) return rc;
+            HIP_TRY(hipEventRecord(c->ev_copy[k], st));   // the caller's stream is done with slot k
+            c->copied[k] = true;
+        } else if (tv) {
+            HIP_TRY(hipEventRecord((*tv)[2], st));
+        }
         c->frames += 1;
         return RT_OK;
     }
-    // pipelined: this frame's gather runs beside the caller's stream's next work (the next
-    // frame's render).  The previous frame is completed here: on rank 0 its unshuffle runs on the
-    // communicator's stream right behind its gather, so the render stream does not wait for it
-    // (only the render into its slot, one frame later, does)
+
+    // rank 0, pipelined.  In the caller's stream order: complete the previous frame (slot j:
+    // wait for its peers' scatter, copy it to rgb8_dev), then render this frame's own tiles into
+    // frame[k] -- which the copy of two frames back read, on this same stream.  On the
+    // communicator's stream: this frame's gather and the scatter of its peers' tiles into
+    // frame[k] (after that old copy, ev_copy[k]).  At world 1 it is the render and one copy.
     if (c->pending >= 0) {
         const int j = c->pending;
-        if (c->rank == 0) {
-            HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_caller, 0));
-            if ((rc = assemble(c, j, rgb8_dev, c->comm_stream)) != RT_OK) return rc;
-            HIP_TRY(hipEventRecord(c->ev_asm[j], c->comm_stream));
-            HIP_TRY(hipStreamWaitEvent(st, c->ev_asm[j], 0));
-        } else {
-            HIP_TRY(hipStreamWaitEvent(st, c->ev_gather[j], 0));
+        if (peers) HIP_TRY(hipStreamWaitEvent(st, c->ev_asm[j], 0));
+        HIP_TRY(hipMemcpyAsync(rgb8_dev, c->frame[j], sizeof(uint32_t) * (size_t)c->W * c->H, hipMemcpyDeviceToDevice, st));
+        if (peers) {
+            HIP_TRY(hipEventRecord(c->ev_copy[j], st));
+            c->copied[j] = true;
         }
         c->frames += 1;
+        c->pending = -1;
     }
-    HIP_TRY(hipEventRecord(c->ev_render[k], st));
-    HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_render[k], 0));
-    if ((rc = gather(c, k, deal, c->comm_stream)) != RT_OK) return rc;
-    HIP_TRY(hipEventRecord(c->ev_gather[k], c->comm_stream));
-    if (tv) HIP_TRY(hipEventRecord((*tv)[2], c->comm_stream));
+    c->slot_deal[k] = c->cur;
+    if ((rc = render(c->frame[k], 0)) != RT_OK) return rc;
+    if (peers) {
+        if (c->copied[k]) HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_copy[k], 0));
+        if ((rc = gather(c, k, deal, c->comm_stream)) != RT_OK) return rc;
+        if (tv) HIP_TRY(hipEventRecord((*tv)[2], c->comm_stream));
+        if ((rc = scatter_peers(c, k, c->frame[k], c->comm_stream)) != RT_OK) return rc;
+        HIP_TRY(hipEventRecord(c->ev_asm[k], c->comm_stream));
+    } else if (tv) {
+        HIP_TRY(hipEventRecord((*tv)[2], st));
+    }
     c->pending = k;
     c->slot = k ^ 1;
     return RT_OK;
@@ -704,7 +840,7 @@ int rt_comm_timing(rt_comm *c, double *render_ms, double *gather_ms, uint64_t *f
         HIP_TRY(hipEventElapsedTime(&x, e[0], e[1]));
         HIP_TRY(hipEventElapsedTime(&y, e[1], e[2]));
         a += x;
-        b += y;
+        b += std::max(0.0f, y);
     }
     *render_ms = a;
     *gather_ms = b;
@@ -716,12 +852,20 @@ int rt_comm_timing(rt_comm *c, double *render_ms, double *gather_ms, uint64_t *f
 int rt_multi_flush(rt_renderer *r, rt_comm *c, uint32_t *rgb8_dev, void *stream) {
     if (!r || !c) return fail(RT_ERR_INVALID, "rt_multi_flush: null argument");
     if (c->pending < 0) return RT_OK;
+    if (c->rank == 0 && !rgb8_dev) return fail(RT_ERR_INVALID, "rt_multi_flush: rank 0 needs an output frame");
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t st = (hipStream_t)stream;
     const int j = c->pending;
-    HIP_TRY(hipStreamWaitEvent(st, c->ev_gather[j], 0));
-    int rc = assemble(c, j, rgb8_dev, st);
-    if (rc != RT_OK) return rc;
+    if (c->rank == 0) {
+        if (c->world > 1) HIP_TRY(hipStreamWaitEvent(st, c->ev_asm[j], 0));
+        HIP_TRY(hipMemcpyAsync(rgb8_dev, c->frame[j], sizeof(uint32_t) * (size_t)c->W * c->H, hipMemcpyDeviceToDevice, st));
+        if (c->world > 1) {
+            HIP_TRY(hipEventRecord(c->ev_copy[j], st));
+            c->copied[j] = true;
+        }
+    } else {
+        HIP_TRY(hipStreamWaitEvent(st, c->ev_gather[j], 0));
+    }
     c->pending = -1;
     c->frames += 1;
     return RT_OK;

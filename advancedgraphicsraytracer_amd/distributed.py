@@ -232,10 +232,11 @@ class NativeShardedFrame:
     def deal_info(self):
         """The deal frames are rendered under now (rt_comm_deal_info): {balanced, tiles, deals_built,
         exchanges, moves, moves_skipped_on_reset}."""
-        b, t, st = C.c_int(), C.c_uint32(), (C.c_uint64 * 4)()
+        b, t, st, h = C.c_int(), C.c_uint32(), (C.c_uint64 * 4)(), C.c_uint64()
         self._check(self.L.rt_comm_deal_info(self.h, C.byref(b), C.byref(t), None, st))
+        self._check(self.L.rt_comm_deal_hash(self.h, C.byref(h)))
         return {"balanced": b.value, "tiles": t.value, "deals_built": int(st[0]), "exchanges": int(st[1]),
-                "moves": int(st[2]), "moves_skipped_on_reset": int(st[3])}
+                "moves": int(st[2]), "moves_skipped_on_reset": int(st[3]), "hash": f"{h.value:016x}"}
 
     def close(self):
         h = getattr(self, "h", None)

@@ -308,6 +308,10 @@ int rt_comm_timing(rt_comm *c, double *render_ms, double *gather_ms, uint64_t *f
  * (room for *ntiles) its global tile indices in render order; stats: [0] balanced deals built,
  * [1] cost exchanges run, [2] accumulator moves run, [3] moves skipped on reset frames. */
 int rt_comm_deal_info(const rt_comm *c, int *balanced, uint32_t *ntiles, uint32_t *tile_list, uint64_t stats[4]);
+/* FNV-1a hash of the deal in use (every rank's tile lists and offsets): equal on every rank, and
+ * in two runs that built the same deal.  Balanced deals are cut on tile costs rounded to 1/64 of
+ * the frame's mean tile cost, so run-to-run noise in the measured cycles rarely moves a cut. */
+int rt_comm_deal_hash(const rt_comm *c, uint64_t *hash);
 
 int rt_renderer_counters(rt_renderer *r, rt_counters *out);
 /* Overlapped primary+shadow frames (RT_PS_PIPELINE; no reference counterpart -- Renderer::Tick,

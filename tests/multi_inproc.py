@@ -19,8 +19,12 @@ MODE: sync | pipelined -- the interleaved deal;
                   frames (level-0 costs: a second balanced deal), primary+shadow again;
       moving   -- balanced, then the camera moves every frame with the accumulator reset (the
                   deal is kept), then a new static camera (rebalanced; the switch frame resets);
-      ptbal    -- path-traced frames only (spp 16, depth 10), balanced on level-0 costs.
-The balanced modes print the communicator's deal_info and require the balanced deal at the end."""
+      ptbal    -- path-traced frames only (spp 16, depth 10), balanced on level-0 costs;
+      fault:<site>:<rank> -- balanced, with RT_MULTI_FAULT=<site>:<rank> (csrc/rt_multi.cpp): that
+                  rank's local step of a per-frame collective fails; every rank must return an
+                  error from the same call and none may be left waiting in the collective.
+The balanced modes print the communicator's deal_info and deal hash (equal on every rank) and
+require the balanced deal at the end."""
 import ctypes as C
 import json
 import os
@@ -56,6 +60,8 @@ def plan_for(mode):
         return static + moving + settle                              # (the rebalancing one) resets
     if mode == "ptbal":
         return [(16, 10, 0, False)] * 10
+    if mode.startswith("fault:"):
+        return [(1, 1, 0, False)] * 40
     raise SystemExit(f"unknown mode {mode}")
 
 
@@ -89,33 +95,47 @@ def rank_main(rank, world, uid, recipe, W, H, mode, plan, results, errors):
         out = torch.zeros(W * H, dtype=torch.int32, device="cuda:0") if rank == 0 else None
         optr = C.c_void_p(out.data_ptr()) if rank == 0 else None
         pipelined = mode != "sync"
-        flags = (rt.MULTI_PIPELINED if pipelined else 0) | (rt.MULTI_BALANCED if mode in BALANCED_MODES else 0)
-        copies, deals = [], []
+        fault = mode.startswith("fault:")
+        flags = (rt.MULTI_PIPELINED if pipelined else 0) | (rt.MULTI_BALANCED if mode in BALANCED_MODES or fault else 0)
+        copies, deals, exch = [], [], []
+        failed_at = None
         with torch.cuda.stream(st):
             for f, (spp, depth, shift, reset) in enumerate(plan):
                 cam = camera_for(W, H, shift)
                 p = r.params(spp, depth, f, reset)
-                rt._check(L.rt_render_frame_multi(r.h, h, C.byref(cam), C.byref(p), optr, flags,
-                                                  C.c_void_p(st.cuda_stream)))
+                rc = L.rt_render_frame_multi(r.h, h, C.byref(cam), C.byref(p), optr, flags, C.c_void_p(st.cuda_stream))
+                if fault and rc != 0:   # the injected failure: every rank must see it on this call
+                    failed_at = (f, rc, L.rt_last_error().decode(errors="replace"))
+                    break
+                rt._check(rc)
                 if rank == 0 and (not pipelined or f > 0):
                     copies.append(out.clone())       # on st: no host sync before the next call
-                b = C.c_int()
-                rt._check(L.rt_comm_deal_info(h, C.byref(b), None, None, None))
+                b, stats = C.c_int(), (C.c_uint64 * 4)()
+                rt._check(L.rt_comm_deal_info(h, C.byref(b), None, None, stats))
                 deals.append(b.value)
-            if pipelined:
+                exch.append(int(stats[1]))
+            if pipelined and not fault:
                 rt._check(L.rt_multi_flush(r.h, h, optr, C.c_void_p(st.cuda_stream)))
                 if rank == 0:
                     copies.append(out.clone())
         st.synchronize()
-        b, t, stats = C.c_int(), C.c_uint32(), (C.c_uint64 * 4)()
+        if fault:
+            results[rank] = {"failed_at": failed_at, "frames_ok": len(deals)}
+            rt._check(L.rt_comm_destroy(h))
+            r.close()
+            scene.close()
+            return
+        b, t, stats, dh = C.c_int(), C.c_uint32(), (C.c_uint64 * 4)(), C.c_uint64()
         rt._check(L.rt_comm_deal_info(h, C.byref(b), C.byref(t), None, stats))
+        rt._check(L.rt_comm_deal_hash(h, C.byref(dh)))
         mine = np.zeros(t.value, np.uint32)
         rt._check(L.rt_comm_deal_info(h, None, C.byref(t), mine.ctypes.data_as(C.POINTER(C.c_uint32)), None))
         results[rank] = {"frames": [c.cpu().numpy() for c in copies], "acc": r.accumulator(), "counters": r.counters(),
                          "tiles": mine,
                          "deal": {"balanced": b.value, "tiles": t.value, "deals_built": int(stats[0]),
-                                  "exchanges": int(stats[1]), "moves": int(stats[2]), "moves_skipped": int(stats[3])},
-                         "deal_per_frame": deals}
+                                  "exchanges": int(stats[1]), "moves": int(stats[2]), "moves_skipped": int(stats[3]),
+                                  "hash": f"{dh.value:016x}"},
+                         "deal_per_frame": deals, "exchanges_per_frame": exch}
         rt._check(L.rt_comm_destroy(h))
         r.close()
         scene.close()
@@ -126,6 +146,8 @@ def rank_main(rank, world, uid, recipe, W, H, mode, plan, results, errors):
 def main():
     world, mode, recipe, W, H = int(sys.argv[1]), sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
     plan = plan_for(mode)
+    if mode.startswith("fault:"):
+        os.environ["RT_MULTI_FAULT"] = mode[len("fault:"):]
     L = rt.lib()
     uid = (C.c_uint8 * rt.RT_COMM_ID_BYTES)()
     rt._check(L.rt_comm_unique_id(uid))
@@ -138,7 +160,12 @@ def main():
         t.join(timeout=400)
     if errors or any(t.is_alive() for t in threads):
         print(json.dumps({"ok": False, "errors": errors, "alive": [t.is_alive() for t in threads]}), flush=True)
-        sys.exit(1)
+        os._exit(1)   # a rank left waiting in a collective: do not join it
+    if mode.startswith("fault:"):
+        fails = [results[k]["failed_at"] for k in range(world)]
+        ok = all(x is not None for x in fails) and len({x[0] for x in fails}) == 1
+        print(json.dumps({"ok": ok, "world": world, "mode": mode, "failed_at": fails}), flush=True)
+        sys.exit(0 if ok else 1)
     ref = rt.Renderer(rt.Scene.recipe(recipe), W, H)
     want = []
     for f, (spp, depth, shift, reset) in enumerate(plan):
@@ -159,12 +186,14 @@ def main():
     if mode in BALANCED_MODES and world > 1:
         # every rank ends on the same balanced deal, having built at least one
         deal_ok = all(results[k]["deal"]["balanced"] == 1 and results[k]["deal"]["deals_built"] >= 1 for k in range(world))
+        deal_ok = deal_ok and len({results[k]["deal"]["hash"] for k in range(world)}) == 1   # one deal everywhere
         if mode == "balanced":   # the primary+shadow deal, then a rebalance on path-traced costs (which
             # may cut the frame where the first deal did); every new deal moved the accumulators
             deal_ok = deal_ok and deal["exchanges"] >= 2 and deal["moves"] == deal["deals_built"]
-        if mode == "moving":     # no deal change while the camera moves; a rebalance afterwards
-            per = results[0]["deal_per_frame"]
-            deal_ok = deal_ok and per[30:40] == [per[29]] * 10 and deal["deals_built"] >= 2
+        if mode == "moving":     # no deal change while the camera moves; the new static camera runs a
+            # balancing attempt (which may rebuild the same cut: a valid rebalance either way)
+            per, ex = results[0]["deal_per_frame"], results[0]["exchanges_per_frame"]
+            deal_ok = deal_ok and per[30:40] == [per[29]] * 10 and ex[30:40] == [ex[29]] * 10 and ex[-1] > ex[39]
     ok = len(got) == len(plan) and not bad_frames and not bad_acc and all(sums[key] == c[key] for key in sums) and deal_ok
     print(json.dumps({"ok": ok, "world": world, "mode": mode, "frames": len(got), "bad_frames": bad_frames,
                       "bad_acc_ranks": bad_acc, "counters": sums, "want_counters": {k: c[k] for k in sums},

@@ -52,6 +52,23 @@ def test_multi_frame_world_n_on_one_gpu(world, mode, recipe, W, H):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("site", ["cost_upload:1", "mig_pack:2", "mig_pack:0"])
+def test_collective_failure_reaches_every_rank(site):
+    """A local failure inside a per-frame collective (the cost exchange's block upload, the
+    accumulator move's pack; RT_MULTI_FAULT injects it on one rank) makes rt_render_frame_multi
+    return an error on EVERY rank from the same call -- no rank is left waiting in the group."""
+    assert os.path.exists(STANDIN)
+    env = dict(os.environ, RT_RCCL_LIB=STANDIN)
+    p = subprocess.run([sys.executable, "-u", DRIVER, "3", "fault:" + site, "teapotF", "200", "120"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and lines, f"rc {p.returncode}\n{p.stdout[-2000:]}\n{p.stderr[-2000:]}"
+    res = json.loads(lines[-1])
+    print(json.dumps(res))
+    assert res["ok"], res
+
+
+@pytest.mark.gpu
 def test_balanced_deal_with_default_tune_delay():
     """The bench's setting (RT_TUNE_DELAY_MS unset = 100 ms of GPU time before a renderer times its
     camera walk, so its tile costs come late): the cost exchange is retried (frames 6, 12, 24, ...)

@@ -38,6 +38,8 @@ for s in "$@"; do
         region) step region 300 python tools/timed_region.py --out gpurun_out/timed_region.jsonl ;;
         parity4)   # round 4: the forced wave walk at full size, bit-exact accumulators, the deal machinery
             step parity4 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "wave_walk_config4 or baseline_configs or zero_seed or packet or primary_plus_shadow" -s ;;
+        multinative)
+            step multinative 300 python -u -m pytest tests/test_multi_native.py -m gpu -q -p no:cacheprovider --timeout 240 --timeout-method thread ;;
         multi4)
             step multi4 1100 python -u -m pytest tests/test_multi_inproc.py -m gpu -q -p no:cacheprovider --timeout 520 --timeout-method thread -s ;;
         benchcfg)

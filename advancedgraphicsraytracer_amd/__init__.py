@@ -170,6 +170,7 @@ def lib():
         "rt_renderer_overlap_depth": ([vp, C.POINTER(C.c_int), fp], C.c_int),
         "rt_renderer_device_bytes": ([vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)], C.c_int),
         "rt_renderer_tile_costs": ([vp, C.POINTER(u32), u32, C.POINTER(u32)], C.c_int),
+        "rt_renderer_tile_work": ([vp, C.POINTER(Camera), C.POINTER(FrameParams), C.POINTER(u32), u32, vp, vp], C.c_int),
         "rt_renderer_choices": ([vp, C.POINTER(C.c_int), C.POINTER(C.c_int), fp, fp], C.c_int),
         "rt_renderer_set_walk_check": ([vp, C.c_int], C.c_int),
         "rt_renderer_walk_stats": ([vp, C.POINTER(C.c_uint64)], C.c_int),
@@ -761,6 +762,25 @@ class Renderer:
         if n.value:
             _check(self.L.rt_renderer_tile_costs(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), n.value, C.byref(n)))
         return out
+
+    def tile_work(self, spp=1, depth=None, frame=None, pixels=False, stream=None):
+        """Deterministic work map of one frame (rt_renderer_tile_work, a dry run: nothing rendered):
+        per row-major tile, node visits + primitive tests of its rays.  pixels=True also returns the
+        per-pixel counters [H*W, 4] (closest-hit nodes, closest-hit prims, any-hit nodes, any-hit prims)."""
+        tx, ty = (self.width + 7) // 8, (self.height + 7) // 8
+        work = np.zeros(tx * ty, np.uint32)
+        p = self.params(spp, depth, frame)
+        buf = None
+        if pixels:
+            torch = _torch()
+            buf = torch.zeros(self.width * self.height * 4, dtype=torch.int32, device=f"cuda:{self.scene.device}")
+        _check(self.L.rt_renderer_tile_work(self.h, C.byref(self.camera), C.byref(p),
+                                            work.ctypes.data_as(C.POINTER(C.c_uint32)), len(work),
+                                            None if buf is None else C.c_void_p(buf.data_ptr()),
+                                            None if stream is None else C.c_void_p(stream)))
+        if buf is None:
+            return work
+        return work, buf.view(-1, 4).cpu().numpy().view(np.uint32)
 
     def accumulator(self):
         acc = np.zeros((self.height * self.width, 4), np.float32)

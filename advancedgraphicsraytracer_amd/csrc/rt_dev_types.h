@@ -139,6 +139,8 @@ struct TraceArgs {
 #define RT_DECLARE_LAUNCHERS(NS)                                                                  \
     namespace NS {                                                                                \
     void launch_frame(const SceneView &S, const FrameArgs &F, const FrameLaunch &L);              \
+    void launch_work(const SceneView &S, const FrameArgs &F, const FrameLaunch &L,               \
+                     uint32_t *tile_work, uint32_t *pixel_work);                                  \
     void launch_intersect(const SceneView &S, const rt_ray *rays, rt_hit *hits, uint32_t n,       \
                           size_t lds, hipStream_t st);                                            \
     void launch_occluded(const SceneView &S, const rt_ray *rays, uint8_t *out, uint32_t n,        \

@@ -198,6 +198,8 @@ struct rt_renderer {
     // explicit tile deal of rt_render_shard_tiles (FrameArgs::tile_map): local -> global tile,
     // uploaded when it changes; and rank 0's per-global-tile (shard << 24 | local) for assembly
     std::vector<uint32_t> map_host;
+    uint32_t *d_work = nullptr;     // dry-run work frame: per local tile (work_frame)
+    uint32_t work_cap = 0;
     uint32_t *d_map = nullptr;
     size_t map_cap = 0;
     uint64_t map_hash = 0;
@@ -1139,17 +1141,17 @@ int tune_gate(rt_renderer *r, uint64_t key, hipStream_t st, bool &open) {
     return RT_OK;
 }
 
-int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
-                  uint32_t *out, int packed, void *stream, const uint32_t *tiles = nullptr, uint32_t ntiles_map = 0) {
-    if (!r || !cam || !p || !out) return fail(RT_ERR_INVALID, "rt_render: null argument");
+// The frame record of one rank's part of a frame (camera, size, the interleaved shard or the
+// explicit tile list) -- shared by the frame launch and the dry-run work frame.
+int frame_args(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
+               const uint32_t *tiles, uint32_t ntiles_map, FrameArgs &F) {
     if (p->width != r->W || p->height != r->H)
         return fail(RT_ERR_INVALID, "frame size differs from the renderer's accumulator");
     if (p->spp == 0) return fail(RT_ERR_INVALID, "spp must be >= 1");
     if (p->mode > RT_MODE_PACKET) return fail(RT_ERR_INVALID, "unknown integrator mode");
     if (nshards == 0 || shard >= nshards) return fail(RT_ERR_INVALID, "bad shard index");
-    rt_scene *s = r->scene;
-    HIP_TRY(hipSetDevice(s->device));
-    FrameArgs F{};
+    HIP_TRY(hipSetDevice(r->scene->device));
+    F = FrameArgs{};
     for (int i = 0; i < 3; ++i) {
         F.cam_pos[i] = cam->pos[i]; F.cam_tl[i] = cam->top_left[i];
         F.cam_tr[i] = cam->top_right[i]; F.cam_bl[i] = cam->bottom_left[i];
@@ -1167,10 +1169,62 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         F.ntiles_local = ntiles_map;
         F.tile_map = r->d_map;
     }
-    F.packed_out = packed;
     F.acc = r->d_acc;
-    F.out = out;
     F.counters = r->d_counters;
+    F.nchunks = 1;
+    F.nunits = F.ntiles_local;
+    return RT_OK;
+}
+
+// Dry-run work map (k_render_work) of one rank's part of a frame: per local tile, node visits +
+// primitive tests of its rays summed over lanes and samples, read back to the host (blocking on
+// `st`).  The camera rays take the reference-order lane walk whatever walk the renderer timed,
+// so the map depends on the frame alone.  Path-traced / primary+shadow frames (RT_MODE_PATH) only.
+int work_frame(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
+               const uint32_t *tiles, uint32_t ntiles_map, std::vector<uint32_t> &work, uint32_t *pixel_work,
+               hipStream_t st) {
+    if (!r || !cam || !p) return fail(RT_ERR_INVALID, "work frame: null argument");
+    if (p->mode != RT_MODE_PATH) return fail(RT_ERR_UNSUPPORTED, "work frame: RT_MODE_PATH frames only");
+    if (p->depth > 32) return fail(RT_ERR_UNSUPPORTED, "Trace depth above 32");
+    FrameArgs F;
+    int rc = frame_args(r, cam, p, shard, nshards, tiles, ntiles_map, F);
+    if (rc != RT_OK) return rc;
+    const uint32_t n = F.ntiles_local;
+    work.assign(n, 0u);
+    if (n == 0) return RT_OK;
+    rt_scene *s = r->scene;
+    if (n > r->work_cap) {
+        HIP_TRY(hipDeviceSynchronize());
+        if (r->d_work) HIP_TRY(hipFree(r->d_work));
+        r->d_work = nullptr;
+        r->work_cap = 0;
+        HIP_TRY(hipMalloc(&r->d_work, sizeof(uint32_t) * n));
+        r->work_cap = n;
+    }
+    HIP_TRY(hipMemsetAsync(r->d_work, 0, sizeof(uint32_t) * n, st));
+    SceneView view = s->view;
+    view.wave_primary = 0;
+    view.walk_check = RT_WALK_CHECK_OFF;
+    view.walk_stats = nullptr;
+    const int md = p->depth <= 1 ? 1 : 32;
+    FrameLaunch L{RT_MODE_PATH, md, !s->view.sky_const, dim3((n + 3) / 4), dim3(256), stack_bytes(s), st, 0};
+    if (s->ext) kext::launch_work(view, F, L, r->d_work, pixel_work);
+    else kcore::launch_work(view, F, L, r->d_work, pixel_work);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(work.data(), r->d_work, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return RT_OK;
+}
+
+int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
+                  uint32_t *out, int packed, void *stream, const uint32_t *tiles = nullptr, uint32_t ntiles_map = 0) {
+    if (!r || !cam || !p || !out) return fail(RT_ERR_INVALID, "rt_render: null argument");
+    rt_scene *s = r->scene;
+    FrameArgs F;
+    if (int rc = frame_args(r, cam, p, shard, nshards, tiles, ntiles_map, F); rc != RT_OK) return rc;
+    const uint32_t tiles_x = F.tiles_x, tiles_y = (r->H + 7) / 8, ntiles = tiles_x * tiles_y;
+    F.packed_out = packed;
+    F.out = out;
     if (F.ntiles_local == 0) return RT_OK;
     hipStream_t st = (hipStream_t)stream;
     const uint32_t depth = p->depth;
@@ -1514,6 +1568,14 @@ int rt::render_part(rt_renderer *r, const rt_camera *cam, const rt_frame_params 
     return launch_render(r, cam, p, shard, nshards, out_dev, packed, stream);
 }
 
+int rt::render_work(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
+                    const uint32_t *tiles, uint32_t n, std::vector<uint32_t> &work, void *stream) {
+    if (!r) return fail(RT_ERR_INVALID, "render_work: null renderer");
+    if (tiles || n)
+        return work_frame(r, cam, p, 0, 1, tiles ? tiles : reinterpret_cast<const uint32_t *>(r), n, work, nullptr, (hipStream_t)stream);
+    return work_frame(r, cam, p, shard, nshards, nullptr, 0, work, nullptr, (hipStream_t)stream);
+}
+
 int rt::renderer_geometry(const rt_renderer *r, uint32_t *W, uint32_t *H, int *device) {
     if (!r) return fail(RT_ERR_INVALID, "null renderer");
     *W = r->W;
@@ -1763,6 +1825,7 @@ int rt_renderer_destroy(rt_renderer *r) {
     if (r->d_order) (void)hipFree(r->d_order);
     if (r->d_cost) (void)hipFree(r->d_cost);
     if (r->d_map) (void)hipFree(r->d_map);
+    if (r->d_work) (void)hipFree(r->d_work);
     if (r->d_where) (void)hipFree(r->d_where);
     for (auto &e : r->tev)
         if (e) (void)hipEventDestroy(e);
@@ -1963,6 +2026,18 @@ int rt_renderer_device_bytes(const rt_renderer *r, uint64_t *bytes, uint32_t *ps
     }
     *bytes = b;
     if (ps_buffers) *ps_buffers = nps;
+    return RT_OK;
+}
+
+int rt_renderer_tile_work(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t *work, uint32_t n,
+                          uint32_t *pixel_work_dev, void *stream) {
+    if (!r || !cam || !p || (n && !work)) return fail(RT_ERR_INVALID, "rt_renderer_tile_work: null argument");
+    const uint32_t ntiles = ((r->W + 7) / 8) * ((r->H + 7) / 8);
+    if (n < ntiles) return fail(RT_ERR_INVALID, "rt_renderer_tile_work: room for every tile needed");
+    std::vector<uint32_t> w;
+    int rc = work_frame(r, cam, p, 0, 1, nullptr, 0, w, pixel_work_dev, (hipStream_t)stream);
+    if (rc != RT_OK) return rc;
+    std::memcpy(work, w.data(), sizeof(uint32_t) * w.size());
     return RT_OK;
 }
 

@@ -60,6 +60,12 @@ int accumulator_unpack(rt_renderer *r, const uint32_t *tiles_dev, uint32_t n, co
 int render_part(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
                 const uint32_t *tiles, uint32_t n, int packed, uint32_t *out_dev, void *stream);
 
+// the dry-run work map of the same part of a frame (rt_renderer_tile_work): per local tile, node
+// visits + primitive tests summed over its lanes and samples -- deterministic, the multi-GPU
+// deals' cost input.  Blocks on `stream`.  RT_ERR_UNSUPPORTED for modes other than RT_MODE_PATH.
+int render_work(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
+                const uint32_t *tiles, uint32_t n, std::vector<uint32_t> &work, void *stream);
+
 // SURVEY.md 8(d) scenes as descriptions
 struct SceneSource {
     std::vector<rt_prim> prims;

@@ -379,7 +379,7 @@ constexpr double kCostQuant = 64.0;
 // a rank that could not read its costs, or could not upload its block, still enters the group
 // (its status word says so) and the call then fails on every rank; the deal changes only when
 // every rank measured its tiles (`complete`).  Blocking: O(log frames) calls per parameter set.
-int rebalance(rt_comm *c, rt_renderer *r, DealP &next, bool &complete) {
+int rebalance(rt_comm *c, rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, DealP &next, bool &complete) {
     const Rccl &R = rccl();
     const Deal &cur = *c->cur;
     uint32_t most = 0;
@@ -388,7 +388,18 @@ int rebalance(rt_comm *c, rt_renderer *r, DealP &next, bool &complete) {
     const uint32_t mine = cur.count(c->rank);
     std::vector<uint32_t> block(B, 0u);
     uint32_t have = 0;
-    const int lrc = rt_renderer_tile_costs(r, block.data() + 2, mine, &have);
+    // this rank's tile costs under the current deal: the dry-run work map (deterministic; on the
+    // communicator's stream -- it reads only the scene), else the renderer's measured cycles
+    std::vector<uint32_t> work;
+    int lrc = mine == 0 ? RT_OK
+              : cur.id != 0 ? render_work(r, cam, p, 0, 1, cur.tiles.data() + cur.off[c->rank], mine, work, c->comm_stream)
+                            : render_work(r, cam, p, (uint32_t)c->rank, (uint32_t)c->world, nullptr, 0, work, c->comm_stream);
+    if (lrc == RT_OK && work.size() == mine) {
+        std::copy(work.begin(), work.end(), block.begin() + 2);
+        have = mine;
+    } else if (lrc == RT_ERR_UNSUPPORTED) {
+        lrc = rt_renderer_tile_costs(r, block.data() + 2, mine, &have);
+    }
     bool any = mine == 0;
     for (uint32_t i = 0; i < mine && lrc == RT_OK && have == mine; ++i) any = any || block[2 + i] != 0;
     block[0] = (lrc != RT_OK ? 2u : 0u) | (lrc == RT_OK && have == mine && any ? 1u : 0u);
@@ -713,7 +724,7 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
             }
             if (!c->settled && c->pcalls == c->next_try) {
                 bool complete = false;
-                if ((rc = rebalance(c, r, next, complete)) != RT_OK) return rc;
+                if ((rc = rebalance(c, r, cam, p, next, complete)) != RT_OK) return rc;
                 if (complete) c->settled = true;
                 else c->next_try = c->next_try < (1u << 30) ? 2u * c->next_try : c->next_try;
             }

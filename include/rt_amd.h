@@ -287,11 +287,13 @@ int rt_comm_destroy(rt_comm *c);
 /* RT_MULTI_TIMING: HIP events around this rank's render and its gather, summed by rt_comm_timing */
 #define RT_MULTI_TIMING 2u
 /* RT_MULTI_BALANCED: the ranks render the cost-balanced compact deal of rt_tile_deal instead of
- * t % world once every rank has measured its tiles' costs (rt_renderer_tile_costs: wave cycles of
- * primary+shadow tiles, level-0 cycles of path-traced ones).  A parameter set (camera, size, spp,
- * depth, mode) tries on its 6th frame, then its 12th, 24th, ... until every rank has costs -- one
- * all-gather of [status, costs] blocks, after which every rank builds the same deal -- and not
- * again until a parameter changes; the deal in use is kept across camera moves.  When tiles
+ * t % world.  Costs: the dry-run work map of each rank's tiles (rt_renderer_tile_work's node
+ * visits + primitive tests, deterministic) for RT_MODE_PATH frames; the measured wave cycles
+ * (rt_renderer_tile_costs) for the other modes, once every rank has them.  A parameter set
+ * (camera, size, spp, depth, mode) tries on its 6th frame (then its 12th, 24th, ... while some
+ * rank has no costs) -- one all-gather of [status, costs] blocks, after which every rank builds
+ * the same deal -- and not again until a parameter changes; the deal in use is kept across
+ * camera moves.  When tiles
  * change owner their accumulator values move to the new owner (point-to-point, in stream
  * order), except on frames with reset set, so accumulation goes on exactly.  Frames are
  * identical under any deal; every rank must pass the same flags. */
@@ -309,8 +311,9 @@ int rt_comm_timing(rt_comm *c, double *render_ms, double *gather_ms, uint64_t *f
  * [1] cost exchanges run, [2] accumulator moves run, [3] moves skipped on reset frames. */
 int rt_comm_deal_info(const rt_comm *c, int *balanced, uint32_t *ntiles, uint32_t *tile_list, uint64_t stats[4]);
 /* FNV-1a hash of the deal in use (every rank's tile lists and offsets): equal on every rank, and
- * in two runs that built the same deal.  Balanced deals are cut on tile costs rounded to 1/64 of
- * the frame's mean tile cost, so run-to-run noise in the measured cycles rarely moves a cut. */
+ * in two runs that built the same deal -- every run of the same frames for RT_MODE_PATH deals,
+ * whose costs are the deterministic work map.  (Cycle costs of the other modes are rounded to
+ * 1/64 of the frame's mean tile cost first, so run-to-run noise rarely moves a cut.) */
 int rt_comm_deal_hash(const rt_comm *c, uint64_t *hash);
 
 int rt_renderer_counters(rt_renderer *r, rt_counters *out);
@@ -344,6 +347,16 @@ int rt_renderer_choices(const rt_renderer *r, int *walk, int *split, float walk_
  * frame of a parameter set on).  At most n entries are copied.  Diagnostics and cost-balanced
  * tile deals. */
 int rt_renderer_tile_costs(const rt_renderer *r, uint32_t *costs, uint32_t n, uint32_t *n_out);
+/* Deterministic work map of one whole frame (camera + params as rt_render_frame, RT_MODE_PATH
+ * only): a dry run that traces the frame's rays -- same seeds, camera rays in the reference's
+ * IntersectBVH order -- and writes nothing but counts; the accumulator, the frame count and the
+ * ray counters are untouched.  work[t] (n >= ceil(W/8) * ceil(H/8), row-major tiles) = BVH node
+ * visits + primitive tests of tile t's rays, summed over its pixels and samples.  pixel_work_dev
+ * (device, may be NULL): 4 u32 per pixel -- closest-hit node visits, closest-hit primitive tests,
+ * any-hit (shadow) node visits, any-hit primitive tests.  Blocks on `stream`.  The multi-GPU
+ * deals (RT_MULTI_BALANCED) are cut on this map, so two runs of a frame get the same deal. */
+int rt_renderer_tile_work(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t *work, uint32_t n,
+                          uint32_t *pixel_work_dev, void *stream);
 /* Checks of the wave-coherent camera walk (RT_WALK_WAVE, or RT_WALK_AUTO once timed faster) of a
  * renderer's primary+shadow frames.  The walk always re-traces in the reference order every lane
  * whose result could depend on the visiting order (an exact-distance tie, or a hit nearer than

@@ -78,6 +78,8 @@ def lib():
         L.or_trace_rays.argtypes = [vp, fp, C.c_int, C.POINTER(C.c_uint8), C.c_int, C.POINTER(C.c_uint32), fp,
                                     C.POINTER(Stats)]
         L.or_camera_rays.argtypes = [C.POINTER(Camera), C.c_int, C.c_int, C.c_int, ip, C.c_int, fp]
+        L.or_pixel_work.argtypes = [vp, C.POINTER(Camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.c_int,
+                                    C.POINTER(C.c_uint32)]
         L.or_intersect.argtypes = [vp, fp, C.c_int, fp, ip, fp, fp, C.c_int]
         L.or_intersect_packets.argtypes = [vp, fp, C.c_int, fp, ip, fp, fp]
         L.or_occluded.argtypes = [vp, fp, C.c_int, C.POINTER(C.c_uint8)]
@@ -182,6 +184,15 @@ class Scene:
         self.L.or_trace_pixels(self.h, C.byref(cam), W, H, spp, depth, frame, _p(pixels, C.c_int32), len(pixels),
                                _p(rgb, C.c_float), C.byref(st))
         return rgb, st.as_dict()
+
+    def pixel_work(self, W, H, pixels, spp=1, depth=10, frame=0):
+        """Traversal counters per pixel [n, 4]: closest-hit nodes / prims, any-hit nodes / prims."""
+        pixels = np.ascontiguousarray(pixels, dtype=np.int32)
+        out = np.zeros((len(pixels), 4), np.uint32)
+        cam = self.camera(W, H)
+        self.L.or_pixel_work(self.h, C.byref(cam), W, H, spp, depth, frame, _p(pixels, C.c_int32), len(pixels),
+                             _p(out, C.c_uint32))
+        return out
 
     def trace_rays(self, rays, seeds, depth=10, flags=None):
         """Renderer::Trace / WhittedTrace (set_integrator) on (n, 7) rays with per-ray RNG states;

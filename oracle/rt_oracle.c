@@ -740,13 +740,30 @@ static inline int hits_aabb(const ray_t *r, const node *n) {          /* 414-430
     return tmax >= tmin && tmin < r->t && tmax > 0;
 }
 
+/* Traversal work counters of or_pixel_work (NULL otherwise): per pixel [0] closest-hit node
+ * visits (interior + leaf), [1] closest-hit primitive tests, [2] any-hit node visits, [3] any-hit
+ * primitive tests -- the library's dry-run work map (rt_renderer_tile_work) counts the same. */
+static __thread uint32_t *tl_work;
+
+/* slab entry distance with the reference's selects (intersect_aabb's tmin before the accept test) */
+static inline float slab_entry(const ray_t *r, const node *n) {
+    float tx1 = (n->mn[0] - r->O.x) * r->rD.x, tx2 = (n->mx[0] - r->O.x) * r->rD.x;
+    float tmin = smin(tx1, tx2);
+    float ty1 = (n->mn[1] - r->O.y) * r->rD.y, ty2 = (n->mx[1] - r->O.y) * r->rD.y;
+    tmin = smax(tmin, smin(ty1, ty2));
+    float tz1 = (n->mn[2] - r->O.z) * r->rD.z, tz2 = (n->mx[2] - r->O.z) * r->rD.z;
+    return smax(tmin, smin(tz1, tz2));
+}
+
 static void intersect_bvh(const or_scene *s, ray_t *r, counters *k) {   /* 285-320 */
     const node *n = &s->nodes[0];
     const node *stack[64];
     uint32_t sp = 0;
     if (k) k->isect++;
     for (;;) {
+        if (tl_work) tl_work[0]++;
         if (n->count > 0) {
+            if (tl_work) tl_work[1] += n->count;
             for (uint32_t i = 0; i < n->count; i++) {
                 int oi = (int)s->idx[n->leftFirst + i];
                 prim_intersect(&s->p[oi], r, oi);
@@ -775,10 +792,12 @@ static int is_occluded(const or_scene *s, const ray_t *r, counters *k) {   /* 45
     uint32_t sp = 0;
     if (k) k->occl++;
     for (;;) {
+        if (tl_work) tl_work[2]++;
         if (n->count > 0) {
             for (uint32_t i = 0; i < n->count; i++) {
                 int oi = (int)s->idx[n->leftFirst + i];
                 if (k) { k->prim++; k->prim_o++; }
+                if (tl_work) tl_work[3]++;
                 if (prim_hit(&s->p[oi], r)) return 1;
             }
             if (sp == 0) break;
@@ -788,7 +807,12 @@ static int is_occluded(const or_scene *s, const ray_t *r, counters *k) {   /* 45
         const node *c1 = &s->nodes[n->leftFirst], *c2 = &s->nodes[n->leftFirst + 1];
         int h1 = hits_aabb(r, c1), h2 = hits_aabb(r, c2);
         if (k) { k->aabb += 2; k->aabb_o += 2; }
-        if (h1 && h2) { n = c1; stack[sp++] = c2; }
+        if (h1 && h2) {
+            /* counting (or_pixel_work): the library's child order for shadow rays, the box the ray
+             * enters later first -- the answer is the same bool in any order, only the counts move */
+            if (tl_work && slab_entry(r, c2) > slab_entry(r, c1)) { n = c2; stack[sp++] = c1; }
+            else { n = c1; stack[sp++] = c2; }
+        }
         else if (!(h1 || h2)) { if (sp == 0) break; n = stack[--sp]; }
         else if (h1) n = c1;
         else n = c2;
@@ -1339,6 +1363,18 @@ static f3 trace_pixel(const or_scene *s, const or_camera *c, int W, int H, int s
         res = add(res, s->integrator == 1 ? whitted(s, &r, depth, &seed, k) : trace(s, &r, 1, depth, &seed, k));
     }
     return smul(1.0f / (float)spp, res);
+}
+
+void or_pixel_work(const or_scene *s, const or_camera *c, int W, int H, int spp, int depth, int frame,
+                   const int32_t *pixels, int n, uint32_t *work) {
+    #pragma omp parallel for schedule(dynamic, 16)
+    for (int i = 0; i < n; i++) {
+        uint32_t *w = work + 4 * (size_t)i;
+        w[0] = w[1] = w[2] = w[3] = 0;
+        tl_work = w;
+        (void)trace_pixel(s, c, W, H, spp, depth, frame, pixels[i], NULL);
+        tl_work = NULL;
+    }
 }
 
 void or_trace_pixels(const or_scene *s, const or_camera *c, int W, int H, int spp, int depth, int frame,

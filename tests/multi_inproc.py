@@ -19,7 +19,7 @@ MODE: sync | pipelined -- the interleaved deal;
                   frames (level-0 costs: a second balanced deal), primary+shadow again;
       moving   -- balanced, then the camera moves every frame with the accumulator reset (the
                   deal is kept), then a new static camera (rebalanced; the switch frame resets);
-      ptbal    -- path-traced frames only (spp 16, depth 10), balanced on level-0 costs;
+      ptbal    -- path-traced frames only (spp 16, depth 10), balanced on the dry-run work map;
       fault:<site>:<rank> -- balanced, with RT_MULTI_FAULT=<site>:<rank> (csrc/rt_multi.cpp): that
                   rank's local step of a per-frame collective fails; every rank must return an
                   error from the same call and none may be left waiting in the collective.
@@ -48,9 +48,8 @@ def plan_for(mode):
         # frames, primary+shadow again
         return [(s, d, 0, False) for s, d in [(1, 1)] * 6 + [(2, 1), (1, 3), (2, 4), (1, 1), (1, 1)]]
     if mode == "balanced":
-        # the walk is timed over frames 1-16 and the costs exist from frame 17: the attempts on
-        # frames 6 and 12 find none, the one on frame 24 builds the deal (INPROC_PS_FRAMES: more
-        # primary+shadow frames, for runs with a tuning delay)
+        # the first balancing attempt (frame 6) builds the deal from the dry-run work map
+        # (INPROC_PS_FRAMES: more primary+shadow frames, for runs with a tuning delay)
         n = int(os.environ.get("INPROC_PS_FRAMES", "30"))
         return [(1, 1, 0, False)] * n + [(1, 3, 0, False)] * 10 + [(2, 1, 0, False)] * 3
     if mode == "moving":

@@ -52,6 +52,26 @@ def test_multi_frame_world_n_on_one_gpu(world, mode, recipe, W, H):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world,mode,recipe,W,H", [(3, "balanced", "mig16", 256, 144), (8, "ptbal", "cfg5", 480, 270)])
+def test_balanced_deal_is_reproducible(world, mode, recipe, W, H):
+    """Balanced deals are cut on the dry-run work map (node visits + primitive tests, not wave
+    cycles): two runs of the same frames build the same deal -- equal rt_comm_deal_hash."""
+    assert os.path.exists(STANDIN)
+    env = dict(os.environ, RT_RCCL_LIB=STANDIN)
+    hashes = []
+    for _ in range(2):
+        p = subprocess.run([sys.executable, "-u", DRIVER, str(world), mode, recipe, str(W), str(H)], env=env,
+                           capture_output=True, text=True, timeout=500)
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        assert p.returncode == 0 and lines, f"rc {p.returncode}\n{p.stdout[-2000:]}\n{p.stderr[-2000:]}"
+        res = json.loads(lines[-1])
+        assert res["ok"], res
+        hashes.append(res["deal"]["hash"])
+    print(hashes)
+    assert hashes[0] == hashes[1], hashes
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("site", ["cost_upload:1", "mig_pack:2", "mig_pack:0"])
 def test_collective_failure_reaches_every_rank(site):
     """A local failure inside a per-frame collective (the cost exchange's block upload, the

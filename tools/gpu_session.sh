@@ -38,6 +38,11 @@ for s in "$@"; do
         region) step region 300 python tools/timed_region.py --out gpurun_out/timed_region.jsonl ;;
         parity4)   # round 4: the forced wave walk at full size, bit-exact accumulators, the deal machinery
             step parity4 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "wave_walk_config4 or baseline_configs or zero_seed or packet or primary_plus_shadow" -s ;;
+        worktest)
+            step worktest 300 python -u -m pytest tests/test_work_map.py -m gpu -q -p no:cacheprovider --timeout 240 --timeout-method thread ;;
+        tail)
+            step tail_mig 300 python tools/tail_tiles.py --scene mig16 --json gpurun_out/tail_mig16.json
+            step tail_tp 300 python tools/tail_tiles.py --scene teapotF --json gpurun_out/tail_teapotF.json ;;
         multinative)
             step multinative 300 python -u -m pytest tests/test_multi_native.py -m gpu -q -p no:cacheprovider --timeout 240 --timeout-method thread ;;
         multi4)

@@ -2,8 +2,10 @@
 """Per-rank frame time of bench.py's N > 1 workload, measured on one GPU: every rank's share of
 the frame (its 1/N of the tiles) rendered back to back on a renderer of its own, for N = 1, 2,
 4, 8; the slowest rank bounds the frame.  Predicts the driver's scaling efficiency up to the
-gather.  Deals: "interleaved" (t % N, rt_render_shard) or "balanced" (rt_tile_deal over the
-measured tile costs of a full frame, rt_render_shard_tiles -- what RT_MULTI_BALANCED switches to).
+gather.  Deals: "interleaved" (t % N, rt_render_shard), "balanced" (rt_tile_deal over the
+dry-run work map of a full frame, rt_renderer_tile_work -- what RT_MULTI_BALANCED cuts since round
+5 -- rendered with rt_render_shard_tiles), "balanced_cycles" (the same over the measured wave
+cycles of a full frame, round 4's deal input) or "blocksB" (BxB-tile blocks round-robin).
 Weak scaling: spp = N x --spp per rank; --strong: one frame of --spp split N ways.
 
 usage: shard_time.py [--scene teapotF] [--depth 1] [--spp S] [--strong] [--deal interleaved,balanced]
@@ -68,7 +70,7 @@ def main():
     ap.add_argument("--strong", action="store_true", help="the config's spp per shard (one frame split N ways)")
     ap.add_argument("--spp", type=int, default=1, help="samples per pixel of the whole frame (strong) / per GPU (weak)")
     ap.add_argument("--ns", default="1,2,4,8")
-    ap.add_argument("--deal", default="interleaved", help="comma list: interleaved, balanced")
+    ap.add_argument("--deal", default="interleaved", help="comma list: interleaved, balanced, balanced_cycles, blocksB")
     ap.add_argument("--ranks", default="all", choices=("all", "last"), help="time every rank's share or the last only")
     ap.add_argument("--out", default=None, help="append the summary line to this jsonl file")
     a = ap.parse_args()
@@ -85,7 +87,15 @@ def main():
     r0.close()
     ns = [int(x) for x in a.ns.split(",")]
     full_cost = None
-    if "balanced" in a.deal.split(",") and "interleaved" not in a.deal.split(","):
+    deals = a.deal.split(",")
+    work_map = None
+    if "balanced" in deals:   # the product's deal input: deterministic, no timing needed
+        rw = rt.Renderer(scene, a.w, a.h)
+        work_map = rw.tile_work(spp=a.spp if a.strong else a.spp * ns[0], depth=a.depth, frame=100000)
+        rw.close()
+        q = max(1.0, work_map.mean() / 64.0)          # rt_multi.cpp's 1/64-of-the-mean rounding
+        work_map = np.floor(work_map / q + 0.5).astype(np.uint32)
+    if "balanced_cycles" in deals and "interleaved" not in deals:
         # the balanced deal cuts the measured cost map of a whole frame: measure it first
         spp = a.spp if a.strong else a.spp * ns[0]
         buf = torch.zeros(((a.w + 7) // 8) * ((a.h + 7) // 8) * 64, dtype=torch.int32, device="cuda")
@@ -100,6 +110,8 @@ def main():
             cap = ((a.w + 7) // 8) * ((a.h + 7) // 8) * 64
             buf = torch.zeros(cap, dtype=torch.int32, device="cuda")
             if deal == "balanced":
+                tiles, off = rt.tile_deal(a.w, a.h, n, work_map)
+            elif deal == "balanced_cycles":
                 tiles, off = rt.tile_deal(a.w, a.h, n, full_cost if (full_cost is not None and full_cost.size) else None)
             elif deal.startswith("blocks"):   # blocksB: BxB-tile blocks dealt round-robin (block b -> rank b % n)
                 B = int(deal[6:] or 8)
@@ -114,7 +126,7 @@ def main():
             ranks = range(n) if a.ranks == "all" else [n - 1]
             per = []
             for k in ranks:
-                if deal == "balanced" or deal.startswith("blocks"):
+                if deal.startswith("balanced") or deal.startswith("blocks"):
                     mine = tiles[off[k]:off[k + 1]]
                     render = lambda r, spp_, fr, s, mine=mine: r.render_shard_tiles(buf, mine, spp=spp_, depth=a.depth, frame=fr, stream=s)
                 else:

@@ -71,6 +71,10 @@ struct FrameArgs {
     uint32_t *tile_cost;                // if set: each tile's wave cycles (to build the order)
     float4 *acc;
     uint32_t *out;
+    const uint32_t *fwd_src;            // if set (row-major frames only): each pixel's previous value is
+    uint32_t *fwd_dst;                  // forwarded fwd_src[px] -> fwd_dst[px] as the pixel is stored --
+                                        // the world-1 pipelined multi-GPU frame hands its previous frame
+                                        // to the caller without a copy launch (rt_multi.cpp)
     unsigned long long *counters;       // kCounterSlots slots of 8 u64 (64 B): [0] shadow rays, [1] bounce rays
                                         // ([2..5] the camera walk's counters, SceneView::walk_stats)
 };

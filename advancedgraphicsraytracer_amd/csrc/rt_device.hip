@@ -1217,14 +1217,18 @@ int work_frame(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, u
 }
 
 int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
-                  uint32_t *out, int packed, void *stream, const uint32_t *tiles = nullptr, uint32_t ntiles_map = 0) {
+                  uint32_t *out, int packed, void *stream, const uint32_t *tiles = nullptr, uint32_t ntiles_map = 0,
+                  const uint32_t *fwd_src = nullptr, uint32_t *fwd_dst = nullptr) {
     if (!r || !cam || !p || !out) return fail(RT_ERR_INVALID, "rt_render: null argument");
+    if ((fwd_src || fwd_dst) && (packed || !fwd_src || !fwd_dst)) return fail(RT_ERR_INVALID, "rt_render: bad forward");
     rt_scene *s = r->scene;
     FrameArgs F;
     if (int rc = frame_args(r, cam, p, shard, nshards, tiles, ntiles_map, F); rc != RT_OK) return rc;
     const uint32_t tiles_x = F.tiles_x, tiles_y = (r->H + 7) / 8, ntiles = tiles_x * tiles_y;
     F.packed_out = packed;
     F.out = out;
+    F.fwd_src = fwd_src;
+    F.fwd_dst = fwd_dst;
     if (F.ntiles_local == 0) return RT_OK;
     hipStream_t st = (hipStream_t)stream;
     const uint32_t depth = p->depth;
@@ -1562,10 +1566,13 @@ int rt::accumulator_unpack(rt_renderer *r, const uint32_t *tiles_dev, uint32_t n
 }
 
 int rt::render_part(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
-                    const uint32_t *tiles, uint32_t n, int packed, uint32_t *out_dev, void *stream) {
+                    const uint32_t *tiles, uint32_t n, int packed, uint32_t *out_dev, void *stream,
+                    const uint32_t *fwd_src, uint32_t *fwd_dst) {
     if (!r) return fail(RT_ERR_INVALID, "render_part: null renderer");
-    if (tiles || n) return launch_render(r, cam, p, 0, 1, out_dev, packed, stream, tiles ? tiles : reinterpret_cast<const uint32_t *>(r), n);
-    return launch_render(r, cam, p, shard, nshards, out_dev, packed, stream);
+    if (tiles || n)
+        return launch_render(r, cam, p, 0, 1, out_dev, packed, stream, tiles ? tiles : reinterpret_cast<const uint32_t *>(r), n,
+                             fwd_src, fwd_dst);
+    return launch_render(r, cam, p, shard, nshards, out_dev, packed, stream, nullptr, 0, fwd_src, fwd_dst);
 }
 
 int rt::render_work(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,

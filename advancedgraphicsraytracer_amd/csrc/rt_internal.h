@@ -56,9 +56,12 @@ int accumulator_unpack(rt_renderer *r, const uint32_t *tiles_dev, uint32_t n, co
 // one rank's part of a multi-GPU frame (rt_multi.cpp): the interleaved shard `shard` of
 // `nshards`, or the explicit tile list `tiles` (n tiles; n == 0 with tiles != NULL: none),
 // written packed ([local tile][64], rt_render_shard's layout) or, packed == 0, straight into a
-// row-major W x H frame at the tiles' own pixels (rank 0 renders its tiles into the output frame)
+// row-major W x H frame at the tiles' own pixels (rank 0 renders its tiles into the output frame).
+// fwd_src / fwd_dst (row-major only, may be NULL): as each pixel is stored, its value in fwd_src is
+// first forwarded to fwd_dst (the previous frame handed to the caller within the same launch)
 int render_part(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t shard, uint32_t nshards,
-                const uint32_t *tiles, uint32_t n, int packed, uint32_t *out_dev, void *stream);
+                const uint32_t *tiles, uint32_t n, int packed, uint32_t *out_dev, void *stream,
+                const uint32_t *fwd_src = nullptr, uint32_t *fwd_dst = nullptr);
 
 // the dry-run work map of the same part of a frame (rt_renderer_tile_work): per local tile, node
 // visits + primitive tests summed over its lanes and samples -- deterministic, the multi-GPU

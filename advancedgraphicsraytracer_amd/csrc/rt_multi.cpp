@@ -750,11 +750,13 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
         }
         tv = &c->tev[c->tev_used++];
     }
-    auto render = [&](uint32_t *out, int packed) -> int {
+    auto render = [&](uint32_t *out, int packed, const uint32_t *fwd_src = nullptr, uint32_t *fwd_dst = nullptr) -> int {
         if (tv) HIP_TRY(hipEventRecord((*tv)[0], st));
         int e = deal.id != 0
-                    ? render_part(r, cam, p, 0, 1, deal.tiles.data() + deal.off[c->rank], deal.count(c->rank), packed, out, st)
-                    : render_part(r, cam, p, (uint32_t)c->rank, (uint32_t)c->world, nullptr, 0, packed, out, st);
+                    ? render_part(r, cam, p, 0, 1, deal.tiles.data() + deal.off[c->rank], deal.count(c->rank), packed, out, st,
+                                  fwd_src, fwd_dst)
+                    : render_part(r, cam, p, (uint32_t)c->rank, (uint32_t)c->world, nullptr, 0, packed, out, st, fwd_src,
+                                  fwd_dst);
         if (e != RT_OK) return e;
         if (tv) HIP_TRY(hipEventRecord((*tv)[1], st));
         return RT_OK;
@@ -812,7 +814,20 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
     // wait for its peers' scatter, copy it to rgb8_dev), then render this frame's own tiles into
     // frame[k] -- which the copy of two frames back read, on this same stream.  On the
     // communicator's stream: this frame's gather and the scatter of its peers' tiles into
-    // frame[k] (after that old copy, ev_copy[k]).  At world 1 it is the render and one copy.
+    // frame[k] (after that old copy, ev_copy[k]).  At world 1 the previous frame is complete when
+    // rendered and covers every pixel: the render stores each pixel of frame[k] after forwarding
+    // the same pixel of frame[j] to rgb8_dev (FrameArgs::fwd_*) -- no copy launch, one launch per
+    // frame as in Tick (a separate 8 MB copy cost ~8 us per 1080p frame, profiles/r05/session1).
+    if (!peers && c->pending >= 0) {
+        const int j = c->pending;
+        c->slot_deal[k] = c->cur;
+        if ((rc = render(c->frame[k], 0, c->frame[j], rgb8_dev)) != RT_OK) return rc;
+        if (tv) HIP_TRY(hipEventRecord((*tv)[2], st));
+        c->frames += 1;
+        c->pending = k;
+        c->slot = k ^ 1;
+        return RT_OK;
+    }
     if (c->pending >= 0) {
         const int j = c->pending;
         if (peers) HIP_TRY(hipStreamWaitEvent(st, c->ev_asm[j], 0));

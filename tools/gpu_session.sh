@@ -24,6 +24,9 @@ for s in "$@"; do
         shard)     # per-rank frame times of the N > 1 workloads on one GPU (tools/shard_time.py)
             step shard_mig 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --deal interleaved,balanced --out gpurun_out/shard_time.jsonl
             step shard_tp 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene teapotF --deal interleaved,balanced --out gpurun_out/shard_time.jsonl ;;
+        shardr5)   # round 5: the work-map deal against interleaving / the cycle deal
+            step shard_mig_r5 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --deal balanced,balanced_cycles --out gpurun_out/shard_time.jsonl
+            step shard_cfg5_r5 600 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --ns 8 --deal balanced,interleaved --ranks all --out gpurun_out/shard_time.jsonl ;;
         shard5)
             step shard_cfg5 900 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --deal interleaved,balanced --ranks all --out gpurun_out/shard_time.jsonl
             step shard_cfg3 900 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg3 --depth 4 --spp 4 --warm 6 --frames 6 --deal interleaved,balanced --ranks all --out gpurun_out/shard_time.jsonl ;;

@@ -27,6 +27,13 @@ for s in "$@"; do
         shardr5)   # round 5: the work-map deal against interleaving / the cycle deal
             step shard_mig_r5 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --deal balanced,balanced_cycles --out gpurun_out/shard_time.jsonl
             step shard_cfg5_r5 600 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --ns 8 --deal balanced,interleaved --ranks all --out gpurun_out/shard_time.jsonl ;;
+        c5hwq)     # config 5's 1/8 shard (last rank, interleaved) against hardware queues and slots
+            for q in 8 12 16; do
+                step c5_hwq$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/c5hwq.jsonl
+            done
+            step c5_slots4 300 env GPU_MAX_HW_QUEUES=8 RT_PT_SLOTS=4 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/c5hwq.jsonl
+            step c5_trace 300 env GPU_MAX_HW_QUEUES=8 rocprofv3 --kernel-trace --stats -d gpurun_out/c5tr -o run --output-format csv -- python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved
+            step c5_trsum 60 bash -c "python tools/trace_frames.py gpurun_out/c5tr/run_kernel_trace.csv --tail 0.5 --json gpurun_out/c5tr.json" ;;
         shard5)
             step shard_cfg5 900 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --deal interleaved,balanced --ranks all --out gpurun_out/shard_time.jsonl
             step shard_cfg3 900 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg3 --depth 4 --spp 4 --warm 6 --frames 6 --deal interleaved,balanced --ranks all --out gpurun_out/shard_time.jsonl ;;
@@ -46,6 +53,11 @@ for s in "$@"; do
         tail)
             step tail_mig 300 python tools/tail_tiles.py --scene mig16 --json gpurun_out/tail_mig16.json
             step tail_tp 300 python tools/tail_tiles.py --scene teapotF --json gpurun_out/tail_teapotF.json ;;
+        ohtrace)   # kernel trace of the world-1 multi frame against Tick, serial frames (the idle gaps per frame)
+            for sc in mig16 teapotF; do
+                step ohtr_$sc 300 env GPU_MAX_HW_QUEUES=8 RT_PS_PIPELINE=0 rocprofv3 --kernel-trace --stats -d gpurun_out/ohtr_$sc -o run --output-format csv -- python tools/multi_overhead.py --scene $sc --frames 400 --warm 200 --events none
+                step ohtr_sum_$sc 60 bash -c "python tools/trace_frames.py \$(ls gpurun_out/ohtr_$sc/*/run_kernel_trace.csv gpurun_out/ohtr_$sc/run_kernel_trace.csv 2>/dev/null | head -1) --tail 0.24 --json gpurun_out/ohtr_$sc.json"
+            done ;;
         multinative)
             step multinative 300 python -u -m pytest tests/test_multi_native.py -m gpu -q -p no:cacheprovider --timeout 240 --timeout-method thread ;;
         multi4)

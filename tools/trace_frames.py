@@ -40,13 +40,24 @@ def main():
         else:
             cur_e = max(cur_e, e)
     union += cur_e - cur_s
+    # idle gaps of the GPU between busy intervals (all matching kernels merged)
+    gaps, end = [], rows[0][1]
+    for s, e, _ in rows[1:]:
+        if s > end:
+            gaps.append((s - end) / 1e3)
+        end = max(end, e)
     total = sum(e - s for s, e, _ in rows)
     by = {}
     for s, e, n in rows:
         short = re.sub(r"\(.*", "", n)[:80]
         by.setdefault(short, []).append((s, e))
     out = {"launches": len(rows), "span_ms": span / 1e6, "busy_frac": union / span if span else 0.0,
-           "mean_concurrency": total / union if union else 0.0, "kernels": {}}
+           "mean_concurrency": total / union if union else 0.0,
+           "idle_gaps_us": {"count": len(gaps), "total": round(sum(gaps), 1),
+                            "mean": round(statistics.mean(gaps), 2) if gaps else 0.0,
+                            "max": round(max(gaps), 2) if gaps else 0.0,
+                            "over_10us": sum(1 for g in gaps if g > 10.0)},
+           "kernels": {}}
     for n, iv in sorted(by.items(), key=lambda kv: -sum(e - s for s, e in kv[1])):
         d = [(e - s) / 1e6 for s, e in iv]
         starts = [s for s, _ in iv]

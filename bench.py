@@ -25,9 +25,10 @@ import sys
 import time
 
 
-def _wants_8_queues(argv):
-    """Path tracing (trace depth > 1) or config 4, for this command line (--config / --depth),
-    before anything loads HIP."""
+def _queues_wanted(argv, world):
+    """Hardware queues this command line (--config / --depth) wants, before anything loads HIP:
+    16 for config 5 split over N > 1 ranks, 8 for path tracing (trace depth > 1), config 4 and any
+    N > 1 run, else None (the environment's / HIP's default)."""
     cfg, depth = 2, None
     for i, a in enumerate(argv):
         key, _, val = a.partition("=")
@@ -37,7 +38,10 @@ def _wants_8_queues(argv):
             cfg = int(val)
         elif key == "--depth":
             depth = int(val)
-    return (depth if depth is not None else {3: 4, 5: 10}.get(cfg, 1)) > 1 or cfg == 4
+    pt = (depth if depth is not None else {3: 4, 5: 10}.get(cfg, 1)) > 1
+    if cfg == 5 and pt and world > 1:
+        return 16
+    return 8 if (pt or cfg == 4 or world > 1) else None
 
 
 # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process (4 by default).  Path
@@ -49,17 +53,22 @@ def _wants_8_queues(argv):
 # 0.128 either way; profiles/r02/multi_overhead_hwq8.log).  Config 4 at N = 1 too: its frames in
 # flight (up to 6 renderer streams) no longer share queues -- 0.3045 / 0.3005 -> 0.280 / 0.270 ms
 # (profiles/r03/hwq_ab/).  Config 2 keeps HIP's default: with 8 queues its timed choice drifted to
-# 2 frames in flight and the frame to 0.108-0.120 ms.  Set before HIP initialises.
+# 2 frames in flight and the frame to 0.108-0.120 ms.  Config 5 at N > 1 (each rank a 1/N shard of
+# 4 M paths, 8 path-state slots = 8 renderer streams beside the caller's and the communicator's):
+# 16 queues, 1/8 shard 1.219 / 1.205 -> 1.152 / 1.162 ms interleaved A/B (profiles/r05/c5/
+# hwqab.jsonl; config 4 / 2 shards neutral; config 3 at N = 1 slower with 16).  Set before HIP
+# initialises.
 # The box may export its own value (HIP's default is 4): the bench sets 8 explicitly where its
 # design needs it and records the value in effect (config.hip_hw_queues).  --hw-queues N
 # overrides; never above 32 (the pool refuses more).
 _HWQ_BEFORE = os.environ.get("GPU_MAX_HW_QUEUES")
 _HWQ_ARG = next((a.partition("=")[2] or (sys.argv[i + 2] if i + 2 < len(sys.argv) else "")
                  for i, a in enumerate(sys.argv[1:]) if a.startswith("--hw-queues")), None)
+_HWQ_WANT = _queues_wanted(sys.argv[1:], int(os.environ.get("WORLD_SIZE", "1")))
 if _HWQ_ARG:
     os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, int(_HWQ_ARG))))
-elif _wants_8_queues(sys.argv[1:]) or int(os.environ.get("WORLD_SIZE", "1")) > 1:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+elif _HWQ_WANT:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_HWQ_WANT)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

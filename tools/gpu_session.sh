@@ -34,6 +34,14 @@ for s in "$@"; do
             step c5_slots4 300 env GPU_MAX_HW_QUEUES=8 RT_PT_SLOTS=4 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/c5hwq.jsonl
             step c5_trace 300 env GPU_MAX_HW_QUEUES=8 rocprofv3 --kernel-trace --stats -d gpurun_out/c5tr -o run --output-format csv -- python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved
             step c5_trsum 60 bash -c "python tools/trace_frames.py gpurun_out/c5tr/run_kernel_trace.csv --tail 0.5 --json gpurun_out/c5tr.json" ;;
+        hwqab)     # interleaved A/B of 8 vs 16 hardware queues on the N > 1 shards and config 5 / 3 at N = 1
+            for q in 8 16 8 16; do
+                step ab_c5_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/hwqab.jsonl
+                step ab_mig_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene mig16 --strong --ns 8 --ranks all --deal balanced --out gpurun_out/hwqab.jsonl
+                step ab_tp_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene teapotF --ns 8 --ranks last --deal interleaved --out gpurun_out/hwqab.jsonl
+                step ab_b5_q$q 300 python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline --hw-queues $q
+                step ab_b3_q$q 300 python bench.py --config 3 --steps 30 --warmup 3 --no-cpu-baseline --hw-queues $q
+            done ;;
         shard5)
             step shard_cfg5 900 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --deal interleaved,balanced --ranks all --out gpurun_out/shard_time.jsonl
             step shard_cfg3 900 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg3 --depth 4 --spp 4 --warm 6 --frames 6 --deal interleaved,balanced --ranks all --out gpurun_out/shard_time.jsonl ;;

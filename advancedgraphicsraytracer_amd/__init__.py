@@ -766,21 +766,22 @@ class Renderer:
     def tile_work(self, spp=1, depth=None, frame=None, pixels=False, stream=None):
         """Deterministic work map of one frame (rt_renderer_tile_work, a dry run: nothing rendered):
         per row-major tile, node visits + primitive tests of its rays.  pixels=True also returns the
-        per-pixel counters [H*W, 4] (closest-hit nodes, closest-hit prims, any-hit nodes, any-hit prims)."""
+        per-pixel counters [H*W, 8] (closest-hit nodes, closest-hit prims, any-hit nodes, any-hit prims,
+        closest-hit pops of interior / leaf entries already beyond the ray's t, 0, 0)."""
         tx, ty = (self.width + 7) // 8, (self.height + 7) // 8
         work = np.zeros(tx * ty, np.uint32)
         p = self.params(spp, depth, frame)
         buf = None
         if pixels:
             torch = _torch()
-            buf = torch.zeros(self.width * self.height * 4, dtype=torch.int32, device=f"cuda:{self.scene.device}")
+            buf = torch.zeros(self.width * self.height * 8, dtype=torch.int32, device=f"cuda:{self.scene.device}")
         _check(self.L.rt_renderer_tile_work(self.h, C.byref(self.camera), C.byref(p),
                                             work.ctypes.data_as(C.POINTER(C.c_uint32)), len(work),
                                             None if buf is None else C.c_void_p(buf.data_ptr()),
                                             None if stream is None else C.c_void_p(stream)))
         if buf is None:
             return work
-        return work, buf.view(-1, 4).cpu().numpy().view(np.uint32)
+        return work, buf.view(-1, 8).cpu().numpy().view(np.uint32)
 
     def accumulator(self):
         acc = np.zeros((self.height * self.width, 4), np.float32)

@@ -352,9 +352,12 @@ int rt_renderer_tile_costs(const rt_renderer *r, uint32_t *costs, uint32_t n, ui
  * IntersectBVH order -- and writes nothing but counts; the accumulator, the frame count and the
  * ray counters are untouched.  work[t] (n >= ceil(W/8) * ceil(H/8), row-major tiles) = BVH node
  * visits + primitive tests of tile t's rays, summed over its pixels and samples.  pixel_work_dev
- * (device, may be NULL): 4 u32 per pixel -- closest-hit node visits, closest-hit primitive tests,
- * any-hit (shadow) node visits, any-hit primitive tests.  Blocks on `stream`.  The multi-GPU
- * deals (RT_MULTI_BALANCED) are cut on this map, so two runs of a frame get the same deal. */
+ * (device, may be NULL): 8 u32 per pixel -- [0] closest-hit node visits, [1] closest-hit primitive
+ * tests, [2] any-hit (shadow) node visits, [3] any-hit primitive tests, [4] / [5] closest-hit
+ * pops of an interior / leaf stack entry whose pushed entry distance is >= the ray's t at the pop
+ * ([4]: pair loads an exact pop-time cull would skip; 0 for trees deeper than 28), [6] [7] 0.
+ * Blocks on `stream`.  The multi-GPU deals (RT_MULTI_BALANCED) are cut on this map, so two runs
+ * of a frame get the same deal. */
 int rt_renderer_tile_work(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, uint32_t *work, uint32_t n,
                           uint32_t *pixel_work_dev, void *stream);
 /* Checks of the wave-coherent camera walk (RT_WALK_WAVE, or RT_WALK_AUTO once timed faster) of a

@@ -186,9 +186,10 @@ class Scene:
         return rgb, st.as_dict()
 
     def pixel_work(self, W, H, pixels, spp=1, depth=10, frame=0):
-        """Traversal counters per pixel [n, 4]: closest-hit nodes / prims, any-hit nodes / prims."""
+        """Traversal counters per pixel [n, 8]: closest-hit nodes / prims, any-hit nodes / prims,
+        closest-hit pops of interior / leaf entries already beyond the ray's t, 0, 0."""
         pixels = np.ascontiguousarray(pixels, dtype=np.int32)
-        out = np.zeros((len(pixels), 4), np.uint32)
+        out = np.zeros((len(pixels), 8), np.uint32)
         cam = self.camera(W, H)
         self.L.or_pixel_work(self.h, C.byref(cam), W, H, spp, depth, frame, _p(pixels, C.c_int32), len(pixels),
                              _p(out, C.c_uint32))

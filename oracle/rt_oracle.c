@@ -742,7 +742,9 @@ static inline int hits_aabb(const ray_t *r, const node *n) {          /* 414-430
 
 /* Traversal work counters of or_pixel_work (NULL otherwise): per pixel [0] closest-hit node
  * visits (interior + leaf), [1] closest-hit primitive tests, [2] any-hit node visits, [3] any-hit
- * primitive tests -- the library's dry-run work map (rt_renderer_tile_work) counts the same. */
+ * primitive tests, [4] / [5] closest-hit pops of an interior / leaf entry whose entry distance
+ * (at its push, IntersectAABB's tmin) is >= the ray's t at the pop -- the library's dry-run work
+ * map (rt_renderer_tile_work) counts the same. */
 static __thread uint32_t *tl_work;
 
 /* slab entry distance with the reference's selects (intersect_aabb's tmin before the accept test) */
@@ -758,6 +760,7 @@ static inline float slab_entry(const ray_t *r, const node *n) {
 static void intersect_bvh(const or_scene *s, ray_t *r, counters *k) {   /* 285-320 */
     const node *n = &s->nodes[0];
     const node *stack[64];
+    float sdist[64];   /* counting only: each entry's IntersectAABB distance at its push */
     uint32_t sp = 0;
     if (k) k->isect++;
     for (;;) {
@@ -771,6 +774,7 @@ static void intersect_bvh(const or_scene *s, ray_t *r, counters *k) {   /* 285-3
             if (k) k->prim += n->count;
             if (sp == 0) break;
             n = stack[--sp];
+            if (tl_work && sdist[sp] >= r->t) tl_work[n->count > 0 ? 5 : 4]++;
             continue;
         }
         const node *c1 = &s->nodes[n->leftFirst], *c2 = &s->nodes[n->leftFirst + 1];
@@ -780,9 +784,10 @@ static void intersect_bvh(const or_scene *s, ray_t *r, counters *k) {   /* 285-3
         if (d1 == 1e30f) {
             if (sp == 0) break;
             n = stack[--sp];
+            if (tl_work && sdist[sp] >= r->t) tl_work[n->count > 0 ? 5 : 4]++;
         } else {
             n = c1;
-            if (d2 != 1e30f) stack[sp++] = c2;
+            if (d2 != 1e30f) { sdist[sp] = d2; stack[sp++] = c2; }
         }
     }
 }
@@ -1369,8 +1374,8 @@ void or_pixel_work(const or_scene *s, const or_camera *c, int W, int H, int spp,
                    const int32_t *pixels, int n, uint32_t *work) {
     #pragma omp parallel for schedule(dynamic, 16)
     for (int i = 0; i < n; i++) {
-        uint32_t *w = work + 4 * (size_t)i;
-        w[0] = w[1] = w[2] = w[3] = 0;
+        uint32_t *w = work + 8 * (size_t)i;
+        for (int q = 0; q < 8; q++) w[q] = 0;
         tl_work = w;
         (void)trace_pixel(s, c, W, H, spp, depth, frame, pixels[i], NULL);
         tl_work = NULL;

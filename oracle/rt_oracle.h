@@ -112,9 +112,11 @@ void or_primary_hits(const or_scene *s, const or_camera *c, int W, int H, int fr
 /* Renderer::Trace radiance averaged over spp for a pixel list (renderer.cpp:17-72, 222) */
 void or_trace_pixels(const or_scene *s, const or_camera *c, int W, int H, int spp, int depth, int frame,
                      const int32_t *pixels, int n, float *rgb, or_stats *st);
-/* Traversal work of a pixel list (integrator 0 / 1): per pixel 4 counters -- closest-hit node
+/* Traversal work of a pixel list (integrator 0 / 1): per pixel 8 counters -- closest-hit node
  * visits (interior + leaf) and primitive tests, any-hit node visits and primitive tests (shadow
- * rays counted in the library's farther-box-first order) -- summed over the pixel's samples */
+ * rays counted in the library's farther-box-first order), closest-hit pops of interior / leaf
+ * entries whose pushed entry distance is >= the ray's t at the pop, 0, 0 -- summed over the
+ * pixel's samples */
 void or_pixel_work(const or_scene *s, const or_camera *c, int W, int H, int spp, int depth, int frame,
                    const int32_t *pixels, int n, uint32_t *work);
 /* One Renderer::Tick over rows [y0,y1): trace, running average into acc (float4 per

@@ -20,7 +20,7 @@ def torch():
 
 def tile_sums(px_work, W, H):
     tx, ty = (W + 7) // 8, (H + 7) // 8
-    tot = px_work.astype(np.int64).sum(axis=1).reshape(H, W)
+    tot = px_work[:, :4].astype(np.int64).sum(axis=1).reshape(H, W)
     pad = np.zeros((ty * 8, tx * 8), np.int64)
     pad[:H, :W] = tot
     return pad.reshape(ty, 8, tx, 8).sum(axis=(1, 3)).reshape(-1)
@@ -43,6 +43,9 @@ def test_work_map_equals_oracle_counts(rt, oracle, torch, recipe, W, H, spp, dep
     assert bad.size == 0, f"{bad.size} pixels differ, first {bad[:5]}: gpu {px[bad[:3]]} oracle {want[bad[:3]]}"
     assert np.array_equal(work.astype(np.int64), tile_sums(want, W, H))
     assert want[:, 0].min() >= spp            # every sample visits the root
+    # the exact pop-time cull's ceiling (counters [4] / [5]): printed for DESIGN.md
+    print(f"{recipe}: pops of interior entries beyond t = {want[:, 4].sum() / max(1, want[:, 0].sum()):.4f} of "
+          f"closest-hit node visits, leaf entries {want[:, 5].sum() / max(1, want[:, 0].sum()):.4f}")
     r.close()
 
 
@@ -82,3 +85,4 @@ def test_oracle_pixel_work_counts(oracle, rt):
     assert np.array_equal(a, b)
     assert a[:, 0].min() >= 2
     assert (a[:, 2] > 0).any()                # some shadow rays
+    assert (a[:, 4] > 0).any() and not a[:, 6:].any()

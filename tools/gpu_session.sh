@@ -60,7 +60,9 @@ for s in "$@"; do
             step worktest 300 python -u -m pytest tests/test_work_map.py -m gpu -q -p no:cacheprovider --timeout 240 --timeout-method thread ;;
         tail)
             step tail_mig 300 python tools/tail_tiles.py --scene mig16 --json gpurun_out/tail_mig16.json
-            step tail_tp 300 python tools/tail_tiles.py --scene teapotF --json gpurun_out/tail_teapotF.json ;;
+            step tail_tp 300 python tools/tail_tiles.py --scene teapotF --json gpurun_out/tail_teapotF.json
+            step tail_c3 300 python tools/tail_tiles.py --scene cfg3 --spp 4 --depth 4 --json gpurun_out/tail_cfg3.json
+            step tail_c5 300 python tools/tail_tiles.py --scene cfg5 --spp 16 --depth 10 --json gpurun_out/tail_cfg5.json ;;
         ohtrace)   # kernel trace of the world-1 multi frame against Tick, serial frames (the idle gaps per frame)
             for sc in mig16 teapotF; do
                 step ohtr_$sc 300 env GPU_MAX_HW_QUEUES=8 RT_PS_PIPELINE=0 rocprofv3 --kernel-trace --stats -d gpurun_out/ohtr_$sc -o run --output-format csv -- python tools/multi_overhead.py --scene $sc --frames 400 --warm 200 --events none

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--w", type=int, default=1920)
     ap.add_argument("--h", type=int, default=1080)
     ap.add_argument("--top", type=int, default=32)
+    ap.add_argument("--spp", type=int, default=1)
+    ap.add_argument("--depth", type=int, default=1, help="> 1: path-traced frames (cycles = level-0 cost map)")
     ap.add_argument("--walk", choices=("lane", "auto"), default="lane",
                     help="camera walk of the rendered frames (lane: the order the work map counts)")
     ap.add_argument("--json", default=None)
@@ -47,13 +49,13 @@ def main():
     f, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < 1.0 or r.tile_costs().size == 0:   # past the tuning gate: costs recorded
         for _ in range(20):
-            r.Tick(out, spp=1, depth=1, frame=0, stream=st.cuda_stream)
+            r.Tick(out, spp=a.spp, depth=a.depth, frame=0, stream=st.cuda_stream)
             f += 1
         torch.cuda.synchronize()
         if time.perf_counter() - t0 > 20:
             break
     cyc = r.tile_costs().astype(np.float64)
-    work, px = r.tile_work(spp=1, depth=1, frame=0, pixels=True)
+    work, px = r.tile_work(spp=a.spp, depth=a.depth, frame=0, pixels=True)
     tx, ty = (W + 7) // 8, (H + 7) // 8
 
     def tiles(v):
@@ -63,7 +65,7 @@ def main():
 
     cam_n, cam_p, sh_n, sh_p = (tiles(px[:, k].astype(np.int64)) for k in range(4))
     chain = cam_n + sh_n
-    res = {"scene": a.scene, "size": [W, H], "frames_rendered": f, "walk": a.walk,
+    res = {"scene": a.scene, "size": [W, H], "spp": a.spp, "depth": a.depth, "frames_rendered": f, "walk": a.walk,
            "cycles_mean": round(float(cyc.mean()), 1), "cycles_max": int(cyc.max()),
            "chain_mean_lane": round(float(chain.mean()), 2), "chain_max_lane": int(chain.max())}
     top = np.argsort(-cyc)[:a.top]
@@ -84,6 +86,11 @@ def main():
     preds = {"work_sum": work.astype(np.float64), "chain_max_lane": chain.max(axis=1).astype(np.float64),
              "chain_sum": chain.sum(axis=1).astype(np.float64)}
     res["corr_with_cycles"] = {k: round(float(np.corrcoef(v, cyc)[0, 1]), 4) for k, v in preds.items()}
+    # the exact pop-time cull's ceiling: closest-hit pops of entries already beyond the ray's t
+    ch = float(px[:, 0].sum())
+    res["pop_cull_ceiling"] = {"interior_pops_beyond_t_over_ch_visits": round(float(px[:, 4].sum()) / ch, 4),
+                               "leaf_pops_beyond_t_over_ch_visits": round(float(px[:, 5].sum()) / ch, 4),
+                               "ch_visits_over_all_visits": round(ch / float(px[:, 0].sum() + px[:, 2].sum()), 4)}
     top_share = {}
     for k, v in preds.items():   # overlap of the top-N by cycles and by the predictor
         tp = set(np.argsort(-v)[:a.top].tolist())

@@ -134,6 +134,9 @@ struct rt_renderer {
     hipEvent_t sev[8] = {};     // split timing: events 2i, 2i+1 around timing frame i
     float split_ms[4] = {};
     int tune = 0;                   // camera walk: 0 warm-up, 1 .. kWalkTimed timed frames, kTuneDecide, kTuneDone
+    hipEvent_t stall_ev = nullptr;  // after the previous frame while a timed group runs (kTuneRestarts)
+    bool stall_armed = false;
+    int walk_restarts = 0, split_restarts = 0, ps_restarts = 0;
     bool wave = false;
     uint64_t tune_key = 0;          // the parameter set whose frames the walk timing ran on
     int walk_check = RT_WALK_CHECK_OFF;     // rt_renderer_set_walk_check
@@ -155,6 +158,7 @@ struct rt_renderer {
     // renderer streams: the path tracer's two path streams are 0 and 1; overlapped primary+
     // shadow frames use the first `depth` of them (frames in flight)
     hipStream_t pt_stream[kPsMaxDepth] = {};
+    int nstreams = 0;               // pt_stream[0 .. nstreams) created (ensure_pipe_streams)
 
     hipEvent_t pt_lv[kPsMaxDepth] = {};   // a renderer stream's work of this frame is done
     hipEvent_t pt_fin[kPtMaxSlots + 1] = {};   // the finish that read d_res[b] is done
@@ -230,6 +234,15 @@ inline bool tuned_alternative(const float ms[4]) {
 }
 constexpr int kWalkTimed = 4 * kTuneGroup;
 constexpr int kTuneDecide = 1 + kWalkTimed, kTuneDone = kTuneDecide + 1;
+// A timed group assumes frames submitted back to back.  When the caller synchronises inside a
+// group (bench.py's clock ramp every 20 frames, multi_overhead.py every 50), the GPU idles between
+// two of its frames and the group times the host, not the frames: TEAPOT-F 1080p with 8 hardware
+// queues timed its first serial group at 2.48 ms against 1.58 for the last, picked 2 frames in
+// flight and ran at 0.0995 ms against 0.097 serial (round 5, profiles/r05/hwq/).  So while a group
+// runs, an event after each frame is queried when the next frame is submitted: if the previous
+// frame had already completed, the GPU ran dry in between and the group restarts (at most
+// kTuneRestarts times per choice, so a caller that syncs every frame still gets a decision).
+constexpr int kTuneRestarts = 8;
 
 // LDS stack entries per lane: a traversal pushes at most one entry per tree level, so the tree
 // depth is enough.  Rounding it up to 8 cost occupancy where the stacks bound the workgroups
@@ -702,16 +715,21 @@ int set_tile_map(rt_renderer *r, const uint32_t *tiles, uint32_t n, uint32_t nti
 // follows frame n + 1's levels on the caller's stream; slots + 1 buffers let a frame start
 // behind the finish of the frame `slots` back.
 
-// The renderer's two overlap streams and their ordering events (created once).
-int ensure_pipe_streams(rt_renderer *r) {
-    if (r->pt_stream[0]) return RT_OK;
-    for (int k = 0; k < kPsMaxDepth; ++k) {
+// The renderer's overlap streams 0 .. n-1 and their ordering events, created as first needed.
+// Only as many as a mode uses: each stream becomes a hardware queue of its own (up to
+// GPU_MAX_HW_QUEUES), and with 8 queues, creating all 8 streams for a timing that used 2 left
+// TEAPOT-F's frames slow for the next ~50 frames -- the first two frames-in-flight groups timed
+// 2.5-3.1 / 2.2 ms against 1.5 / 1.6 for the last two (round 5, profiles/r05/hwq).
+int ensure_pipe_streams(rt_renderer *r, int n) {
+    n = std::min(n, kPsMaxDepth);
+    if (!r->pt_fin[0])
+        for (int k = 0; k <= kPtMaxSlots; ++k)
+            HIP_TRY(hipEventCreateWithFlags(&r->pt_fin[k], hipEventDisableTiming | hipEventReleaseToDevice));
+    for (int k = r->nstreams; k < n; ++k) {
         HIP_TRY(hipStreamCreateWithFlags(&r->pt_stream[k], hipStreamNonBlocking));
         // ordering between streams of this device only: a device-scope release
         HIP_TRY(hipEventCreateWithFlags(&r->pt_lv[k], hipEventDisableTiming | hipEventReleaseToDevice));
-    }
-    for (int k = 0; k <= kPtMaxSlots; ++k) {
-        HIP_TRY(hipEventCreateWithFlags(&r->pt_fin[k], hipEventDisableTiming | hipEventReleaseToDevice));
+        r->nstreams = k + 1;
     }
     return RT_OK;
 }
@@ -784,8 +802,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     if (pipe && r->pt_serial_last) HIP_TRY(hipStreamSynchronize(st));
     r->pt_serial_last = !pipe;
     if (pipe) {
-        int rc = ensure_pipe_streams(r);
-        if (rc != RT_OK) return rc;
+        int rc = RT_OK;
         if (need > r->pt_need) {
             // as many slots as fit beside 8 GB of headroom (at least 2), decided again whenever a
             // frame needs larger slots: every pending frame is done, slots past the count freed
@@ -821,6 +838,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         }
         par = r->pt_parity;
         r->pt_parity = (par + 1) % (int)(r->pt_nslots + 1);
+        if ((rc = ensure_pipe_streams(r, (int)r->pt_nslots)) != RT_OK) return rc;
         if ((rc = ensure_res(r, par, res_need)) != RT_OK) return rc;
     }
     bool used[kPtMaxSlots] = {};
@@ -996,7 +1014,7 @@ void frame_build(const rt_renderer *r, const SceneView &view, const FrameArgs &F
 }
 
 int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, bool split_ok, bool gate_open,
-                    int &split_ev0, int &split_ev1) {
+                    bool stalled, int &split_ev0, int &split_ev1) {
     split_ev0 = split_ev1 = -1;
     const uint32_t n = F.ntiles_local;
     if (key != r->order_key || n != r->order_n) {
@@ -1005,6 +1023,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
         r->host_cost.clear();
         r->tail_bound = false;
         r->ps_phase = 0;   // the overlap decision belongs to the parameter set too
+        r->ps_restarts = 0;
         if (n != r->order_n) {
             HIP_TRY(hipDeviceSynchronize());                             // frames may still read them
             if (r->d_order) HIP_TRY(hipFree(r->d_order));
@@ -1075,6 +1094,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
         r->order_state = 2;
         r->use_split = k > 0 && r->scene->heavy_split > 0;            // a forced count: no timing
         r->split_phase = (k > 0 && r->scene->heavy_split < 0) ? 0 : -1;
+        r->split_restarts = 0;
         if (r->split_phase == 0 && !r->sev[0])
             for (auto &e : r->sev) HIP_TRY(hipEventCreate(&e));
     }
@@ -1086,6 +1106,10 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
             r->use_split = split = tuned_alternative(r->split_ms);
             r->split_phase = -1;
         } else if (r->split_phase >= 0 && gate_open) {
+            if (stalled && r->split_phase % kTuneGroup != 0 && r->split_restarts < kTuneRestarts) {
+                r->split_phase -= r->split_phase % kTuneGroup;                 // redo the group
+                ++r->split_restarts;
+            }
             const int g = r->split_phase / kTuneGroup, i = r->split_phase % kTuneGroup;   // plain, split, split, plain
             split = g == 1 || g == 2;
             split_ev0 = i == 0 ? 2 * g : -1;
@@ -1318,6 +1342,12 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     const uint64_t pkey = param_key(r, F, cam, p);
     bool gate_open = false;
     if (int rc = tune_gate(r, pkey, st, gate_open); rc != RT_OK) return rc;
+    // did the GPU run dry since the previous frame?  (a timed group then restarts: kTuneRestarts)
+    bool stalled = false;
+    if (r->stall_armed) {
+        stalled = hipEventQuery(r->stall_ev) == hipSuccess;
+        r->stall_armed = false;
+    }
     // camera-ray walk (only the global-node primary+shadow kernel has both)
     const bool walk_kernel = mode == RT_MODE_PATH && md == 1 && !s->ext;
     int walk_ev0 = -1, walk_ev1 = -1;   // tev recorded before / after this launch
@@ -1327,7 +1357,10 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     // frames: a set change in the middle (a multi-GPU deal switch, a camera move) restarts them
     if (walk_kernel && s->walk == RT_WALK_AUTO && r->tune >= 1 && r->tune < kTuneDecide && pkey != r->tune_key)
         r->tune = 0;
-    if (r->tune == 0) r->tune_key = pkey;
+    if (r->tune == 0) {
+        r->tune_key = pkey;
+        r->walk_restarts = 0;
+    }
     const bool walk_pending = walk_kernel && s->walk == RT_WALK_AUTO && r->tune < kTuneDone;
     if (walk_kernel) {
         if (s->walk == RT_WALK_WAVE) view.wave_primary = 1;
@@ -1336,6 +1369,10 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
                 if (!r->tev[0])
                     for (auto &e : r->tev) HIP_TRY(hipEventCreate(&e));
                 if (r->tune >= 1) {   // groups lane, wave, wave, lane
+                    if (stalled && (r->tune - 1) % kTuneGroup != 0 && r->walk_restarts < kTuneRestarts) {
+                        r->tune -= (r->tune - 1) % kTuneGroup;             // redo the group from its first frame
+                        ++r->walk_restarts;
+                    }
                     const int g = (r->tune - 1) / kTuneGroup, i = (r->tune - 1) % kTuneGroup;
                     view.wave_primary = (g == 1 || g == 2) ? 1 : 0;
                     if (i == 0) walk_ev0 = 2 * g;
@@ -1359,7 +1396,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         // half-tile units: primary+shadow frames of the global-node kernel, whole-tile units only
         const bool split_ok = mode == RT_MODE_PATH && md == 1 && F.nchunks <= 1;
         const int rc = tile_order_step(r, F, pkey, cost_map >= 0 ? cost_map : walk_decided ? 2 : walk_pending ? 3 : -1,
-                                       split_ok, gate_open, split_ev0, split_ev1);
+                                       split_ok, gate_open, stalled, split_ev0, split_ev1);
         if (rc != RT_OK) return rc;
         L.grid = dim3((F.nunits + 3) / 4);
     }
@@ -1414,7 +1451,10 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         if (r->ps_phase == 0) r->ps_groups = deep_ok ? 8 : 4;
         const int NG = r->ps_groups;
         const uint32_t *depths = NG == 8 ? kDeep : kShallow;
-        if (r->ps_phase > 0 && r->ps_phase < NG * G && r->frames != r->ps_last + 1) r->ps_phase = 0;   // interrupted
+        if (r->ps_phase > 0 && r->ps_phase < NG * G && r->frames != r->ps_last + 1) {   // interrupted
+            r->ps_phase = 0;
+            r->ps_restarts = 0;
+        }
         if (r->ps_phase > 0 && r->ps_phase == NG * G) {
             HIP_TRY(hipEventSynchronize(r->pev[2 * NG - 1]));
             for (int g = 0; g < NG; ++g) HIP_TRY(hipEventElapsedTime(&r->ps_ms[g], r->pev[2 * g], r->pev[2 * g + 1]));
@@ -1442,11 +1482,15 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
             if (r->ps_phase == 0) {   // streams, events and every result buffer before the timing
                 if (!r->pev[0])
                     for (auto &e : r->pev) HIP_TRY(hipEventCreate(&e));
-                int rc = ensure_pipe_streams(r);
                 const uint32_t maxd = NG == 8 ? 6u : 2u;
+                int rc = ensure_pipe_streams(r, (int)maxd);
                 const uint32_t nb = s->ps_buffers ? s->ps_buffers : maxd + 1u;
                 for (uint32_t k = 0; k < nb && rc == RT_OK; ++k) rc = ensure_ps_res(r, k, ps_bytes);
                 if (rc != RT_OK) return rc;
+            }
+            if (stalled && r->ps_phase % G != 0 && r->ps_restarts < kTuneRestarts) {
+                r->ps_phase -= r->ps_phase % G;                                // redo the group
+                ++r->ps_restarts;
             }
             const int g = r->ps_phase / G;
             depth_k = depths[g];
@@ -1463,7 +1507,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     uint32_t buf = 0;
     int lane_st = 0;
     if (ps_pipe) {
-        int rc = ensure_pipe_streams(r);
+        int rc = ensure_pipe_streams(r, (int)depth_k);
         if (rc != RT_OK) return rc;
         // frame n's kernel on renderer stream n % depth, its samples in buffer n % buffers: with
         // depth + 1 buffers frame n + depth + 1 waits for frame n's finishing pass only, which
@@ -1482,7 +1526,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
             if (!r->ps_join) HIP_TRY(hipEventCreateWithFlags(&r->ps_join, hipEventDisableTiming | hipEventReleaseToDevice));
             HIP_TRY(hipEventRecord(r->ps_join, st));
             if (ps_ev0 >= 0)
-                for (int k = 0; k < kPsMaxDepth; ++k) HIP_TRY(hipStreamWaitEvent(r->pt_stream[k], r->ps_join, 0));
+                for (int k = 0; k < r->nstreams; ++k) HIP_TRY(hipStreamWaitEvent(r->pt_stream[k], r->ps_join, 0));
             else
                 HIP_TRY(hipStreamWaitEvent(L.stream, r->ps_join, 0));
         }
@@ -1515,6 +1559,12 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     }
     if (ps_ev0 >= 0) HIP_TRY(hipEventRecord(r->pev[ps_ev0], st));
     if (ps_ev1 >= 0) HIP_TRY(hipEventRecord(r->pev[ps_ev1], st));
+    // a timed group is running: mark this frame's completion for the next submission's stall check
+    if ((r->tune >= 1 && r->tune < kTuneDecide) || r->split_phase >= 0 || (s->ps_pipeline < 0 && r->ps_phase > 0)) {
+        if (!r->stall_ev) HIP_TRY(hipEventCreateWithFlags(&r->stall_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(r->stall_ev, st));
+        r->stall_armed = true;
+    }
     (void)tiles_y;
     r->primary += frame_pixels(r, F, shard, nshards, tiles_x, ntiles) * p->spp;
     r->frames += 1;
@@ -1844,6 +1894,7 @@ int rt_renderer_destroy(rt_renderer *r) {
         if (e) (void)hipEventDestroy(e);
     if (r->ps_join) (void)hipEventDestroy(r->ps_join);
     if (r->cost_ev) (void)hipEventDestroy(r->cost_ev);
+    if (r->stall_ev) (void)hipEventDestroy(r->stall_ev);
     for (int b = 0; b < kPsMaxDepth + 1; ++b) {
         if (r->ps_res[b]) (void)hipFree(r->ps_res[b]);
         if (r->ps_fin[b]) (void)hipEventDestroy(r->ps_fin[b]);

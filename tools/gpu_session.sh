@@ -42,6 +42,22 @@ for s in "$@"; do
                 step ab_b5_q$q 300 python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline --hw-queues $q
                 step ab_b3_q$q 300 python bench.py --config 3 --steps 30 --warmup 3 --no-cpu-baseline --hw-queues $q
             done ;;
+        c2hwq)     # config 2 at N = 1: HIP's 4 hardware queues against 8 (what N > 1 ranks use)
+            for q in 4 8 4 8 4 8; do
+                step c2_q$q 300 python bench.py --steps 200 --warmup 5 --no-cpu-baseline --no-companion --no-strong --hw-queues $q
+                grep -h '"value"' gpurun_out/c2_q$q.log >> gpurun_out/c2hwq.jsonl
+            done ;;
+        tphwq)     # config 2's N > 1 per-rank work (TEAPOT-F weak shards, and the world-1 multi frame) with 4 vs 8 queues
+            for q in 4 8 4 8; do
+                step tp_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene teapotF --ns 2,8 --ranks last --deal interleaved --out gpurun_out/tphwq.jsonl
+                step tpoh_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/multi_overhead.py --scene teapotF --frames 400 --events none
+                grep -h '"tick_ms"' gpurun_out/tpoh_q$q.log | sed "s/^/{\"q\": $q, \"r\": /; s/$/}/" >> gpurun_out/tphwq_oh.jsonl
+            done ;;
+        c2delay)   # config 2 with 8 queues: the tuning gate's delay against the first timed groups' drift
+            for d in 100 300 100 300; do
+                step c2_d$d 300 env RT_TUNE_DELAY_MS=$d python bench.py --steps 200 --warmup 5 --no-cpu-baseline --no-companion --no-strong --hw-queues 8
+                grep -h '"value"' gpurun_out/c2_d$d.log | sed "s/^/{\"delay\": $d, \"r\": /; s/$/}/" >> gpurun_out/c2delay.jsonl
+            done ;;
         shard5)
             step shard_cfg5 900 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --deal interleaved,balanced --ranks all --out gpurun_out/shard_time.jsonl
             step shard_cfg3 900 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg3 --depth 4 --spp 4 --warm 6 --frames 6 --deal interleaved,balanced --ranks all --out gpurun_out/shard_time.jsonl ;;

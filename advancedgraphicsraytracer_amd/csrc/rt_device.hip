@@ -172,7 +172,8 @@ struct rt_renderer {
     // four: serial, 2, 2, serial), so that a clock drift cancels -- are timed on the caller's
     // stream (events pev[2g], pev[2g + 1] around group g); the next frame keeps the fastest mode
     // for the parameter set, and the result buffers it does not use are freed
-    int ps_phase = 0;               // 0 .. groups x kPsGroup - 1 timing frames, then decide; -1 decided
+    int ps_phase = 0;               // 0 .. groups x G - 1 timing frames (G = kPsGroup, 2 kPsGroup for 8
+                                    // groups), then decide; -1 decided
     int ps_groups = 0;              // timed groups of this decision (4: serial / 2; 8: serial / 2 / 4 / 6)
     uint32_t ps_use = 0;            // decided: frames in flight (0 = serial)
     uint64_t ps_last = 0;           // r->frames at the last timing frame (any other frame restarts)
@@ -1429,9 +1430,9 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
                        ps_bytes <= (2ull << 30);
     // frames in flight for this frame: 0 = serial, else 2..6 renderer streams
     uint32_t depth_k = (ps_ok && s->ps_pipeline == 1) ? s->ps_depth : 0u;
-    // pev recorded on the caller's stream after this frame: ps_ev0 after a timed group's first
-    // frame, ps_ev1 after its last -- the group is timed from one frame's completion to another's,
-    // G - 1 frame periods at its depth in steady state.  (Events before the first frame timed a
+    // pev recorded on the caller's stream after this frame: ps_ev0 after a timed group's frame
+    // SKIP, ps_ev1 after its last -- the group is timed from one frame's completion to another's,
+    // G - 1 - SKIP frame periods at its depth in steady state.  (Events before the first frame timed a
     // deeper group short: its first kernels start on their streams while the caller's stream still
     // finishes earlier frames; TEAPOT-F shards then picked 4-6 in flight, 0.125-0.144 ms against
     // 0.092 with 2.  Round 4.)
@@ -1447,9 +1448,14 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     static const uint32_t kDeep[8] = {0, 2, 4, 6, 6, 4, 2, 0}, kShallow[4] = {0, 2, 2, 0};
     if (ps_ok && s->ps_pipeline < 0 && !gate_open) depth_k = 0;   // timing not started: serial
     if (ps_ok && s->ps_pipeline < 0 && gate_open) {
-        constexpr int G = kPsGroup;
         if (r->ps_phase == 0) r->ps_groups = deep_ok ? 8 : 4;
         const int NG = r->ps_groups;
+        // a group's first frames fill its pipeline (every renderer stream starts behind the previous
+        // group), and their completions bunch up: timed from the first frame's completion, a 6-deep
+        // group of 16 frames measured 0.23-0.25 ms per frame on mig29 x16 whose 6-deep frames then
+        // ran at 0.272 ms against 0.256 with 4 (round 5).  Deep timings run 32-frame groups and time
+        // them from the completion of frame 8 (23 periods), shallow ones 16 frames from frame 2.
+        const int G = NG == 8 ? 2 * kPsGroup : kPsGroup, SKIP = NG == 8 ? 8 : 2;
         const uint32_t *depths = NG == 8 ? kDeep : kShallow;
         if (r->ps_phase > 0 && r->ps_phase < NG * G && r->frames != r->ps_last + 1) {   // interrupted
             r->ps_phase = 0;
@@ -1494,7 +1500,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
             }
             const int g = r->ps_phase / G;
             depth_k = depths[g];
-            if (r->ps_phase % G == 0) ps_ev0 = 2 * g;
+            if (r->ps_phase % G == SKIP) ps_ev0 = 2 * g;
             if (r->ps_phase % G == G - 1) ps_ev1 = 2 * g + 1;
             r->ps_last = r->frames;
             ++r->ps_phase;

@@ -553,8 +553,10 @@ def main():
         if args.depth == 1:   # RT_PS_PIPELINE: serial or overlapped primary+shadow frames (rank 0)
             groups = [g for g in in_flight[1] if g > 0]
             line["overlapped_frames"] = {"state": overlap[0], "in_flight": in_flight[0], "timed_groups_ms": groups,
-                                         "groups": ("frames in flight serial, 2, 4, 6, 6, 4, 2, serial" if len(groups) == 8
-                                                    else "frames in flight serial, 2, 2, serial") + " (16 frames each)"}
+                                         "groups": ("frames in flight serial, 2, 4, 6, 6, 4, 2, serial (32 frames each, "
+                                                    "timed over their last 23 periods)" if len(groups) == 8
+                                                    else "frames in flight serial, 2, 2, serial (16 frames each, timed over "
+                                                    "their last 13 periods)")}
             if choices is not None:   # walk 0 lane / 1 wave, split 0 plain / 1 half tiles; groups A, B, B, A
                 line["timed_choices"] = choices
             if walk_check is not None:

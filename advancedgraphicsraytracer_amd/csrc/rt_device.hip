@@ -57,6 +57,9 @@ struct rt_scene {
                                 // plain build, 8 = the single-sample one wherever it applies (RT_FRAME_WAVES)
     uint32_t num_cus = 256;     // CUs of the device (resident grids, frames-in-flight rules)
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
+    bool nested = true;         // every child box lies inside its parent's (as floats): the wave walk's
+                                // exactness needs it (the builders' trees always; a caller's prebuilt one
+                                // is checked at rt_scene_create)
     int walk = RT_WALK_LANE;    // camera-ray walk of the global-node primary+shadow kernel
     bool ext = false;           // needs the kext kernels (cubes, quads, textures, non-Light light)
     bool pt_lanes = true;           // levels >= 1 run the lane state machine (RT_PT_LANES=0: k_pt_level)
@@ -640,10 +643,23 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_TUNE_DELAY_MS")) s->tune_delay_ms = (float)std::max(0.0, std::atof(e));
     if (const char *e = std::getenv("RT_PT_MEM_MB"))
         s->pt_mem_bytes = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+    // every child box inside its parent's, compared as floats (the wave walk's pops and its leaf
+    // check rely on it: a child's slab entry is then never below its parent's)
+    for (uint32_t i = 0; i < s->bvh.nodes_used && s->nested; ++i) {
+        if (i == 1) continue;
+        const Node &nd = s->bvh.nodes[i];
+        if (nd.count > 0) continue;
+        for (uint32_t c = nd.leftFirst; c < nd.leftFirst + 2 && s->nested; ++c) {
+            const Node &ch = s->bvh.nodes[c];
+            for (int a = 0; a < 3; ++a)
+                if (!(ch.mn[a] >= nd.mn[a]) || !(ch.mx[a] <= nd.mx[a])) s->nested = false;
+        }
+    }
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
     v.wave_primary = 0;
-    s->walk = s->has_cubes ? RT_WALK_LANE : RT_WALK_AUTO;
-    if (const char *e = std::getenv("RT_WAVE_PRIMARY")) s->walk = std::atoi(e) != 0 && !s->has_cubes ? RT_WALK_WAVE : RT_WALK_LANE;
+    const bool wave_ok = !s->has_cubes && s->nested;
+    s->walk = wave_ok ? RT_WALK_AUTO : RT_WALK_LANE;
+    if (const char *e = std::getenv("RT_WAVE_PRIMARY")) s->walk = std::atoi(e) != 0 && wave_ok ? RT_WALK_WAVE : RT_WALK_LANE;
     v.bounds_finite = 1;
     for (uint32_t i = 0; i < s->bvh.nodes_used && v.bounds_finite; ++i) {
         if (i == 1) continue;
@@ -656,6 +672,11 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 }
 
 size_t stack_bytes(const rt_scene *s) { return (size_t)s->stack_depth * 256u * sizeof(uint32_t); }
+// launches whose camera rays may take the wave walk (SceneView::wave_primary) also hold each wave's
+// uniform stack of node words past the lane stacks (walk_words in rt_kernels.inc): 4 waves x depth
+size_t walk_bytes(const rt_scene *s, const SceneView &v) {
+    return v.wave_primary ? (size_t)s->stack_depth * 4u * sizeof(uint32_t) : 0u;
+}
 // the compiled MAXD class a Trace depth runs in
 int max_depth_class(uint32_t depth) { return depth <= 1 ? 1 : depth <= 4 ? 4 : depth <= 10 ? 10 : 32; }
 // pixels covered by a frame / shard launch (primary rays per sample)
@@ -770,7 +791,8 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     rt_scene *s = r->scene;
     // camera rays of level 0 take the wave-coherent walk when the scene forces it, or when
     // the renderer's primary+shadow frames timed it faster (RT_WALK_AUTO)
-    view.wave_primary = !s->has_cubes && (s->walk == RT_WALK_WAVE || (s->walk == RT_WALK_AUTO && r->tune == kTuneDone && r->wave));
+    view.wave_primary = !s->has_cubes && s->nested &&
+                        (s->walk == RT_WALK_WAVE || (s->walk == RT_WALK_AUTO && r->tune == kTuneDone && r->wave));
     view.walk_stats = r->d_counters;
     view.walk_check = r->walk_check;
     const uint64_t npix = (uint64_t)F.ntiles_local * 64u;
@@ -893,8 +915,9 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
                 if (s->ext) kext::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, X);
                 else kcore::launch_pt_lanes(view, F, P, tex, lds, s->num_cus, X);
             } else {
-                resident = s->ext ? kext::launch_pt_level(view, F, P, tex, lds, s->num_cus, X)
-                                  : kcore::launch_pt_level(view, F, P, tex, lds, s->num_cus, X);
+                const size_t lv = level == 0 ? lds + walk_bytes(s, view) : lds;   // camera rays: the walk's words
+                resident = s->ext ? kext::launch_pt_level(view, F, P, tex, lv, s->num_cus, X)
+                                  : kcore::launch_pt_level(view, F, P, tex, lv, s->num_cus, X);
             }
             if (level >= drain_level) break;           // that launch finished every remaining level
             if (level == 0) P.drain_below = (uint32_t)std::min<double>(4e9, s->pt_drain_rounds * resident);
@@ -1539,6 +1562,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         F.samples = r->ps_res[buf];
     }
     if (ps_ok) r->ps_prev = depth_k;
+    L.lds_bytes = stack_bytes(s) + walk_bytes(s, view);   // the camera walk's word stack when it runs
     frame_build(r, view, F, L, ps_pipe);
     if (walk_ev0 >= 0) HIP_TRY(hipEventRecord(r->tev[walk_ev0], st));
     if (split_ev0 >= 0) HIP_TRY(hipEventRecord(r->sev[split_ev0], st));
@@ -1711,6 +1735,8 @@ int rt_scene_set_camera_walk(rt_scene *s, int walk) {
         return fail(RT_ERR_INVALID, "unknown camera walk");
     if (walk != RT_WALK_LANE && s->has_cubes)
         return fail(RT_ERR_UNSUPPORTED, "the wave walk needs order-independent hits; cubes accept on tmax (Primitive.h:221-233)");
+    if (walk != RT_WALK_LANE && !s->nested)
+        return fail(RT_ERR_UNSUPPORTED, "the wave walk needs every child box inside its parent's (this prebuilt BVH has one outside)");
     s->walk = walk;
     return RT_OK;
 }

@@ -313,6 +313,38 @@ def test_prebuilt_bvh_path(rt, scenes):
     hits_equal(g2.IntersectBVH(rays), o.intersect(rays))
 
 
+def test_wave_walk_needs_nested_boxes(rt, oracle, scenes, torch):
+    """The wave camera walk decides its pops from distances kept at the push and checks hits
+    against their leaf box only: both rely on every child box lying inside its parent's.  A
+    prebuilt BVH with a child box poking out of its parent keeps the per-lane walk (RT_WALK_AUTO
+    falls back, RT_WALK_WAVE is refused) and still renders the oracle's frame."""
+    g, _ = scenes("teapotF")
+    prims, mats = rt.recipe_describe("teapotF")
+    nodes, idx = g.bvh()
+    nodes = np.array(nodes, copy=True)
+    f = nodes.view(np.float32).reshape(len(nodes), 8)
+    u = nodes.view(np.uint32).reshape(len(nodes), 8)
+    lf = int(u[0, 6])                                # the root's first child: enlarge its max x
+    f[lf, 3] = np.float32(f[0, 3] + 1.0)
+    g2 = rt.Scene(prims, mats, bvh=(nodes, idx))
+    o = oracle_scene(rt, oracle, prims, mats, bvh=(nodes, idx))   # the same (non-nested) tree
+    with pytest.raises(rt.RTError) as e:
+        g2.set_camera_walk(rt.WALK_WAVE)
+    assert e.value.code == rt.RT_ERR_UNSUPPORTED
+    g.set_camera_walk(rt.WALK_WAVE)                  # the built tree is nested
+    g.set_camera_walk(rt.WALK_AUTO)
+    W, H = 160, 96
+    r = rt.Renderer(g2, W, H)
+    for fr in range(30):                             # past the walk timing: the lane walk throughout
+        got = r.tick_host(spp=1, depth=1, frame=fr)
+    assert r.choices()["walk"] == 0
+    acc = np.zeros((W * H, 4), np.float32)
+    for fr in range(30):
+        want, _ = o.tick(W, H, acc, spp=1, depth=1, frame=fr)
+    assert np.array_equal(got, want)
+    r.close()
+
+
 def test_invalid_scenes_rejected(rt, torch):
     mats = [rt.material(rt.DIFFUSE, (1, 1, 1))]
     with pytest.raises(rt.RTError) as e:

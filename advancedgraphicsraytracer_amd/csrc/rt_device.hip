@@ -139,7 +139,8 @@ struct rt_renderer {
     int tune = 0;                   // camera walk: 0 warm-up, 1 .. kWalkTimed timed frames, kTuneDecide, kTuneDone
     hipEvent_t stall_ev = nullptr;  // after the previous frame while a timed group runs (kTuneRestarts)
     bool stall_armed = false;
-    int walk_restarts = 0, split_restarts = 0, ps_restarts = 0;
+    int walk_restarts = 0, split_restarts = 0, ps_restarts = 0;   // restarts of group *_rg
+    int walk_rg = -1, split_rg = -1, ps_rg = -1;
     bool wave = false;
     uint64_t tune_key = 0;          // the parameter set whose frames the walk timing ran on
     int walk_check = RT_WALK_CHECK_OFF;     // rt_renderer_set_walk_check
@@ -245,8 +246,8 @@ constexpr int kTuneDecide = 1 + kWalkTimed, kTuneDone = kTuneDecide + 1;
 // flight and ran at 0.0995 ms against 0.097 serial (round 5, profiles/r05/hwq/).  So while a group
 // runs, an event after each frame is queried when the next frame is submitted: if the previous
 // frame had already completed, the GPU ran dry in between and the group restarts (at most
-// kTuneRestarts times per choice, so a caller that syncs every frame still gets a decision).
-constexpr int kTuneRestarts = 8;
+// kTuneRestarts times per group, so a caller that syncs every frame still gets a decision).
+constexpr int kTuneRestarts = 4;
 
 // LDS stack entries per lane: a traversal pushes at most one entry per tree level, so the tree
 // depth is enough.  Rounding it up to 8 cost occupancy where the stacks bound the workgroups
@@ -1048,6 +1049,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
         r->tail_bound = false;
         r->ps_phase = 0;   // the overlap decision belongs to the parameter set too
         r->ps_restarts = 0;
+        r->ps_rg = -1;
         if (n != r->order_n) {
             HIP_TRY(hipDeviceSynchronize());                             // frames may still read them
             if (r->d_order) HIP_TRY(hipFree(r->d_order));
@@ -1119,6 +1121,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
         r->use_split = k > 0 && r->scene->heavy_split > 0;            // a forced count: no timing
         r->split_phase = (k > 0 && r->scene->heavy_split < 0) ? 0 : -1;
         r->split_restarts = 0;
+        r->split_rg = -1;
         if (r->split_phase == 0 && !r->sev[0])
             for (auto &e : r->sev) HIP_TRY(hipEventCreate(&e));
     }
@@ -1130,6 +1133,10 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
             r->use_split = split = tuned_alternative(r->split_ms);
             r->split_phase = -1;
         } else if (r->split_phase >= 0 && gate_open) {
+            if (r->split_phase / kTuneGroup != r->split_rg) {
+                r->split_rg = r->split_phase / kTuneGroup;
+                r->split_restarts = 0;
+            }
             if (stalled && r->split_phase % kTuneGroup != 0 && r->split_restarts < kTuneRestarts) {
                 r->split_phase -= r->split_phase % kTuneGroup;                 // redo the group
                 ++r->split_restarts;
@@ -1384,6 +1391,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     if (r->tune == 0) {
         r->tune_key = pkey;
         r->walk_restarts = 0;
+        r->walk_rg = -1;
     }
     const bool walk_pending = walk_kernel && s->walk == RT_WALK_AUTO && r->tune < kTuneDone;
     if (walk_kernel) {
@@ -1393,6 +1401,10 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
                 if (!r->tev[0])
                     for (auto &e : r->tev) HIP_TRY(hipEventCreate(&e));
                 if (r->tune >= 1) {   // groups lane, wave, wave, lane
+                    if ((r->tune - 1) / kTuneGroup != r->walk_rg) {
+                        r->walk_rg = (r->tune - 1) / kTuneGroup;
+                        r->walk_restarts = 0;
+                    }
                     if (stalled && (r->tune - 1) % kTuneGroup != 0 && r->walk_restarts < kTuneRestarts) {
                         r->tune -= (r->tune - 1) % kTuneGroup;             // redo the group from its first frame
                         ++r->walk_restarts;
@@ -1483,6 +1495,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         if (r->ps_phase > 0 && r->ps_phase < NG * G && r->frames != r->ps_last + 1) {   // interrupted
             r->ps_phase = 0;
             r->ps_restarts = 0;
+        r->ps_rg = -1;
         }
         if (r->ps_phase > 0 && r->ps_phase == NG * G) {
             HIP_TRY(hipEventSynchronize(r->pev[2 * NG - 1]));
@@ -1516,6 +1529,10 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
                 const uint32_t nb = s->ps_buffers ? s->ps_buffers : maxd + 1u;
                 for (uint32_t k = 0; k < nb && rc == RT_OK; ++k) rc = ensure_ps_res(r, k, ps_bytes);
                 if (rc != RT_OK) return rc;
+            }
+            if (r->ps_phase / G != r->ps_rg) {
+                r->ps_rg = r->ps_phase / G;
+                r->ps_restarts = 0;
             }
             if (stalled && r->ps_phase % G != 0 && r->ps_restarts < kTuneRestarts) {
                 r->ps_phase -= r->ps_phase % G;                                // redo the group

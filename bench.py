@@ -253,7 +253,7 @@ def strong_config4(world, rank, device, dist, stream, frames=200, warm_s=1.5, ma
 
     nf, t0 = 0, time.perf_counter()
     while True:
-        for _ in range(50):
+        for _ in range(100):   # long blocks: the renderer's timed groups (up to 32 frames) fit between syncs
             step(nf)
             nf += 1
         drain()
@@ -381,21 +381,37 @@ def main():
 
     # clock ramp (untimed, before the W warm-up steps): blocks of frames until
     # --ramp-seconds have passed; at N > 1 the ranks agree on every block (the per-frame
-    # gather is a collective, so every rank must submit the same frames)
+    # gather is a collective, so every rank must submit the same frames).  The renderer times
+    # its choices (camera walk, split order, frames in flight) during the ramp, on groups of up
+    # to 32 frames submitted back to back, and times a group again when the GPU ran dry inside
+    # it: at N = 1 the host waits only for the block before the previous one (the GPU keeps a
+    # block queued), at N > 1 every block ends in a drain and a host sync, so blocks are long.
     nf = 0
     t_ramp = time.perf_counter()
-    block = 20 if args.depth <= 1 else 2
+    block = 100 if args.depth <= 1 else 4
+    pending = []
     while args.ramp_seconds > 0:
         for _ in range(block):
             step(nf)
             nf += 1
-        drain()
-        torch.cuda.synchronize(device)
-        more = torch.tensor([1 if time.perf_counter() - t_ramp < args.ramp_seconds else 0], device=f"cuda:{device}")
         if dist:
-            dist.all_reduce(more, op=dist.ReduceOp.MIN)
-        if not more.item():
+            drain()
+            torch.cuda.synchronize(device)
+        else:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            pending.append(ev)
+            if len(pending) > 2:
+                pending.pop(0).synchronize()
+        more = 1 if time.perf_counter() - t_ramp < args.ramp_seconds else 0
+        if dist:
+            t_more = torch.tensor([more], device=f"cuda:{device}")
+            dist.all_reduce(t_more, op=dist.ReduceOp.MIN)
+            more = int(t_more.item())
+        if not more:
             break
+    drain()
+    torch.cuda.synchronize(device)
     ramp_frames = nf
     for i in range(args.warmup):
         step(nf)

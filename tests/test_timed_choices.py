@@ -40,16 +40,16 @@ def test_choices_decided_when_the_caller_syncs_every_frame(rt, torch):
 
 
 def test_choices_decided_back_to_back(rt, torch):
-    """The usual caller: frames queued on a stream, an occasional synchronisation (as bench.py's
-    clock ramp does every 20 frames)."""
+    """The usual caller: frames queued on a stream, an occasional synchronisation (every 100
+    frames, as bench.py's multi-GPU clock ramp does)."""
     g = rt.Scene.recipe("teapotF")
     W, H = 640, 360
     r = rt.Renderer(g, W, H)
     out = torch.zeros(W * H, dtype=torch.int32, device="cuda:0")
     st = torch.cuda.Stream()
-    for f in range(400):
+    for f in range(600):
         r.Tick(out, spp=1, depth=1, frame=f, stream=st.cuda_stream)
-        if f % 20 == 19:
+        if f % 100 == 99:
             st.synchronize()
     torch.cuda.synchronize()
     ch = r.choices()

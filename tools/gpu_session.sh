@@ -24,6 +24,32 @@ for s in "$@"; do
         shard)     # per-rank frame times of the N > 1 workloads on one GPU (tools/shard_time.py)
             step shard_mig 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --deal interleaved,balanced --out gpurun_out/shard_time.jsonl
             step shard_tp 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene teapotF --deal interleaved,balanced --out gpurun_out/shard_time.jsonl ;;
+        shardmig)
+            step shard_mig 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --deal balanced --out gpurun_out/shard_mig.jsonl ;;
+        walkab)    # round 5: the wave walk's load-free pops against round 4's reloading pops (forced wave walk, serial frames)
+            export RT_WAVE_PRIMARY=1 RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
+            step walkab_mig 300 python tools/ab.py variants/pop_new.so variants/pop_reload.so --scene mig16 --rounds 9 --frames 30 --check
+            step walkab_tp 300 python tools/ab.py variants/pop_new.so variants/pop_reload.so --scene teapotF --rounds 9 --frames 60 --check
+            step walkab_c5 300 python tools/ab.py variants/pop_new.so variants/pop_reload.so --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
+            step walkab_mig720 300 python tools/ab.py variants/pop_new.so variants/pop_reload.so --scene mig16 --w 1280 --h 720 --rounds 9 --frames 40 --check
+            unset RT_WAVE_PRIMARY RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
+        walkshard) # the same two builds on config 4's balanced shards (per-rank max, N = 4 / 8), interleaved
+            cp advancedgraphicsraytracer_amd/librtamd.so gpurun_out/librtamd.keep.so
+            for v in pop_new pop_reload pop_new pop_reload; do
+                cp variants/$v.so advancedgraphicsraytracer_amd/librtamd.so
+                step ws_$v 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --ns 1,4,8 --deal balanced --out gpurun_out/walkshard_$v.jsonl
+            done
+            cp gpurun_out/librtamd.keep.so advancedgraphicsraytracer_amd/librtamd.so && rm gpurun_out/librtamd.keep.so ;;
+        depth8)    # config 4's 1/8 balanced shards: the timed frames-in-flight choice against forced 4 and 6
+            step d8_auto 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --ns 8 --deal balanced --out gpurun_out/depth8.jsonl
+            step d8_f4 400 env GPU_MAX_HW_QUEUES=8 RT_PS_PIPELINE=1 RT_PS_DEPTH=4 python tools/shard_time.py --scene mig16 --strong --ns 8 --deal balanced --out gpurun_out/depth8.jsonl
+            step d8_f6 400 env GPU_MAX_HW_QUEUES=8 RT_PS_PIPELINE=1 RT_PS_DEPTH=6 python tools/shard_time.py --scene mig16 --strong --ns 8 --deal balanced --out gpurun_out/depth8.jsonl ;;
+        scalarab)  # the wave walk's pairs / leaf records through the scalar cache against vector loads
+            export RT_WAVE_PRIMARY=1 RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
+            step sab_mig 300 python tools/ab.py variants/walk_scalar.so variants/walk_vector.so --scene mig16 --rounds 9 --frames 30 --check
+            step sab_tp 300 python tools/ab.py variants/walk_scalar.so variants/walk_vector.so --scene teapotF --rounds 9 --frames 60 --check
+            step sab_c5 300 python tools/ab.py variants/walk_scalar.so variants/walk_vector.so --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
+            unset RT_WAVE_PRIMARY RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
         shardr5)   # round 5: the work-map deal against interleaving / the cycle deal
             step shard_mig_r5 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --deal balanced,balanced_cycles --out gpurun_out/shard_time.jsonl
             step shard_cfg5_r5 600 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --ns 8 --deal balanced,interleaved --ranks all --out gpurun_out/shard_time.jsonl ;;

@@ -54,7 +54,7 @@ def main():
         while f < a.warm or time.perf_counter() - w0 < a.warm_seconds:
             r.Tick(out, spp=a.spp, depth=a.depth, frame=0, stream=sptr)
             f += 1
-            if f % 50 == 0:
+            if f % 200 == 0:   # rare syncs: the renderer's timed groups (up to 32 frames) run back to back
                 st.synchronize()
         st.synchronize()
         t0 = time.perf_counter()
@@ -70,7 +70,7 @@ def main():
         while f < a.warm or time.perf_counter() - w0 < a.warm_seconds:
             sf.submit(spp=a.spp, depth=a.depth, frame=f, stream=sptr, events=ev)
             f += 1
-            if f % 50 == 0:
+            if f % 200 == 0:   # rare syncs: the renderer's timed groups (up to 32 frames) run back to back
                 st.synchronize()
         sf.flush(stream=sptr)
         st.synchronize()

@@ -33,7 +33,7 @@ def time_share(scene, a, spp, frames, render):
     while f < a.warm or time.perf_counter() - t0 < a.warm_seconds:   # past the renderer's tuning gate
         render(r, spp, f, st.cuda_stream)
         f += 1
-        if f % 20 == 0:
+        if f % 200 == 0:   # rare syncs: the renderer's timed groups (up to 32 frames) run back to back
             torch.cuda.synchronize()
     torch.cuda.synchronize()
     c0 = r.counters()
@@ -47,7 +47,9 @@ def time_share(scene, a, spp, frames, render):
     c1 = r.counters()
     ms = ev[0].elapsed_time(ev[1]) / frames
     rays = sum(c1[k] - c0[k] for k in ("primary", "shadow", "bounce")) / frames
-    out = {"ms": round(ms, 4), "mrays": round(rays / 1e6, 3), "in_flight": r.overlap_depth()[0], "choices": r.choices()}
+    od = r.overlap_depth()
+    out = {"ms": round(ms, 4), "mrays": round(rays / 1e6, 3), "in_flight": od[0], "choices": r.choices(),
+           "in_flight_groups_ms": [round(float(x), 4) for x in od[1]]}
     cost = r.tile_costs().astype(np.float64)
     if cost.size:
         out["tile_cycles_max"] = int(cost.max())
@@ -81,7 +83,7 @@ def main():
     while time.perf_counter() - t0 < 0.5:
         r0.Tick(o0, spp=1, depth=a.depth, frame=f)
         f += 1
-        if f % 20 == 0:
+        if f % 200 == 0:   # rare syncs: the renderer's timed groups (up to 32 frames) run back to back
             torch.cuda.synchronize()
     torch.cuda.synchronize()
     r0.close()

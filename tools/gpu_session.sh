@@ -124,14 +124,16 @@ for s in "$@"; do
             export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0
             for c in ${PROF_CONFIGS:-2 3 4 5}; do
                 # k_render: the plain build (k_render<0, 1, false>) or the 8-wave one (k_render_w8<false>)
-                if [ $c = 2 ] || [ $c = 4 ]; then n=60; k="k_render"; else n=6; k="k_pt_lanes"; fi
-                b="python bench.py --config $c --steps $n --warmup 2 --no-cpu-baseline --no-companion --ramp-seconds 0.3"
+                # primary+shadow: the single-sample build's last 60 launches = the timed steps (the camera
+                # walk check after them runs another kernel); path tracing: the last half of k_pt_lanes
+                if [ $c = 2 ] || [ $c = 4 ]; then n=60; k="k_render_w8"; sel="--last 60"; else n=6; k="k_pt_lanes"; sel="--tail 0.5"; fi
+                b="python bench.py --config $c --steps $n --warmup 2 --no-cpu-baseline --no-companion --no-strong --ramp-seconds 0.3"
                 step prof_c$c 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pc$c/trace -o run --output-format csv -- $b
                 step pmc_c${c}_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pc$c/fetch -o pmc --output-format csv -- $b
                 step pmc_c${c}_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pc$c/write -o pmc --output-format csv -- $b
                 step pmc_c${c}_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d gpurun_out/pc$c/sq -o pmc --output-format csv -- $b
                 step pmc_c${c}_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pc$c/tcc -o pmc --output-format csv -- $b
-                step sum_c$c 60 python tools/roofline.py summarize cfg$c "$k" gpurun_out/pc$c/trace gpurun_out/pc$c/fetch gpurun_out/pc$c/write gpurun_out/pc$c/sq gpurun_out/pc$c/tcc --tail 0.5 --out gpurun_out/pmc_summary.json
+                step sum_c$c 60 python tools/roofline.py summarize cfg$c "$k" gpurun_out/pc$c/trace gpurun_out/pc$c/fetch gpurun_out/pc$c/write gpurun_out/pc$c/sq gpurun_out/pc$c/tcc $sel --out gpurun_out/pmc_summary.json
             done
             unset RT_PS_PIPELINE RT_PT_PIPELINE ;;
         prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 100 --warmup 5 --no-cpu-baseline ;;

@@ -19,7 +19,7 @@ Beside it: HBM bytes per launch (FETCH_SIZE x 2 -- gfx950 counts half of a wide 
 (renamed algorithmic_gbs: node / triangle bytes mostly served by L1/L2, never a fraction).
 
 usage:
-  roofline.py summarize KEY KERNEL_SUBSTR DIR [DIR ...] [--out profiles/pmc_summary.json] [--tail 0.5]
+  roofline.py summarize KEY KERNEL_SUBSTR DIR [DIR ...] [--out profiles/pmc_summary.json] [--tail 0.5 | --last N]
       parse a workload's rocprofv3 runs (kernel-trace stats + PMC passes) under DIRs
   roofline.py show [--summary profiles/pmc_summary.json]
       print every workload's roofline fields, recomputed from the summary
@@ -50,12 +50,15 @@ def _rows(dirs, pattern):
                 yield from csv.DictReader(fh)
 
 
-def summarize(key, kernel, dirs, tail=None):
+def summarize(key, kernel, dirs, tail=None, last=None):
     """Per-launch means of every counter found for kernels whose name contains `kernel`,
     and the kernel-trace average duration (rocprofv3 --stats).  tail (0 < tail <= 1): average
     only the last `tail` fraction of each counter's dispatches (by Dispatch_Id) and, when the
     per-launch kernel trace (*kernel_trace.csv) is there, of the launches -- the steady state
-    after the renderer's untimed ramp and tuning frames (the bench's timed region)."""
+    after the renderer's untimed ramp and tuning frames (the bench's timed region).  last (N):
+    the last N dispatches / launches instead -- exactly the bench's timed steps when the kernel
+    name matches nothing after them (round 5: the clock ramp queues up to 200 frames without a
+    host sync, and under the kernel trace those ramp launches recorded ~2x their duration)."""
     per = {}
     for row in _rows(dirs, "*counter_collection.csv"):
         if kernel not in row.get("Kernel_Name", ""):
@@ -65,6 +68,8 @@ def summarize(key, kernel, dirs, tail=None):
             per.setdefault(name, []).append((int(row.get("Dispatch_Id") or 0), float(row["Counter_Value"])))
 
     def keep(vals):
+        if last:
+            return sorted(vals)[-last:]
         if not tail:
             return vals
         vals = sorted(vals)
@@ -80,8 +85,11 @@ def summarize(key, kernel, dirs, tail=None):
             rec["trace_total_ns"] = float(row["TotalDurationNs"])
             rec["trace_kernel_name"] = row["Name"]
             break
-    if tail:
-        rec["tail"] = tail
+    if tail or last:
+        if last:
+            rec["last"] = last
+        else:
+            rec["tail"] = tail
         launches = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
                     for r in _rows(dirs, "*kernel_trace.csv") if kernel in r.get("Kernel_Name", "")]
         if launches:
@@ -156,12 +164,13 @@ def main():
     a.add_argument("dirs", nargs="+")
     a.add_argument("--out", default=SUMMARY)
     a.add_argument("--tail", type=float, default=None, help="average the last fraction of the dispatches only")
+    a.add_argument("--last", type=int, default=None, help="average the last N dispatches only (the bench's timed steps)")
     b = sub.add_parser("show")
     b.add_argument("--summary", default=SUMMARY)
     args = ap.parse_args()
     if args.cmd == "summarize":
         data = load(args.out)
-        data[args.key] = summarize(args.key, args.kernel, args.dirs, tail=args.tail)
+        data[args.key] = summarize(args.key, args.kernel, args.dirs, tail=args.tail, last=args.last)
         os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
         with open(args.out, "w") as f:
             json.dump(data, f, indent=1, sort_keys=True)

@@ -1056,7 +1056,10 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
             if (r->d_cost) HIP_TRY(hipFree(r->d_cost));
             r->d_order = r->d_cost = nullptr;
             r->order_n = 0;
-            HIP_TRY(hipMalloc(&r->d_order, 3u * n * sizeof(uint32_t)));   // plain order | split order
+            // plain order (n) | split order: n + (parts - 1) x the split tiles -- up to 9 n with 8 parts
+            // and every tile split (RT_SPLIT_PARTS / RT_SPLIT_HEAVY; 3 n overflowed a balanced rank's
+            // short tile list with 4 parts and 500 split tiles, round 5)
+            HIP_TRY(hipMalloc(&r->d_order, 9u * n * sizeof(uint32_t)));
             HIP_TRY(hipMalloc(&r->d_cost, 2u * n * sizeof(uint32_t)));   // one cost map per camera walk
             r->order_n = n;
         }
@@ -1342,7 +1345,7 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
                     if (r->d_cost) HIP_TRY(hipFree(r->d_cost));
                     r->d_order = r->d_cost = nullptr;
                     r->order_n = 0;
-                    HIP_TRY(hipMalloc(&r->d_order, 3u * n * sizeof(uint32_t)));
+                    HIP_TRY(hipMalloc(&r->d_order, 9u * n * sizeof(uint32_t)));
                     HIP_TRY(hipMalloc(&r->d_cost, 2u * n * sizeof(uint32_t)));
                     r->order_n = n;
                 }

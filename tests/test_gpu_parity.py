@@ -725,11 +725,13 @@ def test_measured_tile_order_keeps_frames(rt, torch, monkeypatch, recipe, spp, m
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("recipe,shards", [("mig16", 1), ("teapotF", 3)])
+@pytest.mark.parametrize("recipe,shards", [("mig16", 1), ("teapotF", 3), ("mig16", 8)])
 @pytest.mark.parametrize("parts", ["4", "8"])
 def test_split_parts_keep_frames(rt, torch, monkeypatch, recipe, shards, parts):
     """The costliest tiles split into 4 or 8 waves of 16 / 8 lanes (RT_SPLIT_PARTS, forced with
-    RT_SPLIT_HEAVY=64, XCD-grouped for mig16) give the frames of the unordered kernel: 12 frames."""
+    RT_SPLIT_HEAVY=64, XCD-grouped for mig16) give the frames of the unordered kernel: 12 frames.
+    A 1/8 shard of 200x120 holds 47 tiles: every one of them split (the order then holds 9x the
+    tile count; round 5 found 3x allocated)."""
     W, H = 200, 120
     monkeypatch.setenv("RT_TILE_ORDER", "0")
     s_a = rt.Scene.recipe(recipe)

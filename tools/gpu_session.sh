@@ -50,6 +50,12 @@ for s in "$@"; do
             step sab_tp 300 python tools/ab.py variants/walk_scalar.so variants/walk_vector.so --scene teapotF --rounds 9 --frames 60 --check
             step sab_c5 300 python tools/ab.py variants/walk_scalar.so variants/walk_vector.so --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
             unset RT_WAVE_PRIMARY RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
+        splitab8)  # config 4's 1/8 balanced shards: heavy tiles split into 2 / 4 / 8 parts, and more of them
+            step sp8_def 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --ns 8 --deal balanced --out gpurun_out/splitab8.jsonl
+            step sp8_p4 400 env GPU_MAX_HW_QUEUES=8 RT_SPLIT_PARTS=4 python tools/shard_time.py --scene mig16 --strong --ns 8 --deal balanced --out gpurun_out/splitab8.jsonl
+            step sp8_p8 400 env GPU_MAX_HW_QUEUES=8 RT_SPLIT_PARTS=8 python tools/shard_time.py --scene mig16 --strong --ns 8 --deal balanced --out gpurun_out/splitab8.jsonl
+            step sp8_h500 400 env GPU_MAX_HW_QUEUES=8 RT_SPLIT_HEAVY=500 python tools/shard_time.py --scene mig16 --strong --ns 8 --deal balanced --out gpurun_out/splitab8.jsonl
+            step sp8_p4h500 400 env GPU_MAX_HW_QUEUES=8 RT_SPLIT_PARTS=4 RT_SPLIT_HEAVY=500 python tools/shard_time.py --scene mig16 --strong --ns 8 --deal balanced --out gpurun_out/splitab8.jsonl ;;
         shardr5)   # round 5: the work-map deal against interleaving / the cycle deal
             step shard_mig_r5 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --deal balanced,balanced_cycles --out gpurun_out/shard_time.jsonl
             step shard_cfg5_r5 600 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 6 --frames 6 --ns 8 --deal balanced,interleaved --ranks all --out gpurun_out/shard_time.jsonl ;;

@@ -810,17 +810,18 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
         return RT_OK;
     }
 
-    // rank 0, pipelined.  In the caller's stream order: complete the previous frame (slot j:
-    // wait for its peers' scatter, copy it to rgb8_dev), then render this frame's own tiles into
-    // frame[k] -- which the copy of two frames back read, on this same stream.  On the
-    // communicator's stream: this frame's gather and the scatter of its peers' tiles into
-    // frame[k] (after that old copy, ev_copy[k]).  At world 1 the previous frame is complete when
-    // rendered and covers every pixel: the render stores each pixel of frame[k] after forwarding
-    // the same pixel of frame[j] to rgb8_dev (FrameArgs::fwd_*) -- no copy launch, one launch per
-    // frame as in Tick (a separate 8 MB copy cost ~8 us per 1080p frame, profiles/r05/session1).
-    if (!peers && c->pending >= 0) {
-        const int j = c->pending;
-        c->slot_deal[k] = c->cur;
+    // rank 0, pipelined.  On the caller's stream: this frame's own tiles into frame[k] (which the
+    // copy of two frames back read, earlier on this same stream), then the completion of the
+    // previous frame (slot j: wait for its peers' scatter, copy it to rgb8_dev) -- behind the render,
+    // so the render never waits for the peers.  On the communicator's stream: this frame's gather
+    // and the scatter of its peers' tiles into frame[k] (after that old copy, ev_copy[k]).  At
+    // world 1 the previous frame is complete when rendered and covers every pixel: the render stores
+    // each pixel of frame[k] after forwarding the same pixel of frame[j] to rgb8_dev
+    // (FrameArgs::fwd_*) -- no copy launch, one launch per frame as in Tick (a separate 8 MB copy
+    // cost ~8 us per 1080p frame, profiles/r05/session1).
+    const int j = c->pending;
+    c->slot_deal[k] = c->cur;
+    if (!peers && j >= 0) {
         if ((rc = render(c->frame[k], 0, c->frame[j], rgb8_dev)) != RT_OK) return rc;
         if (tv) HIP_TRY(hipEventRecord((*tv)[2], st));
         c->frames += 1;
@@ -828,18 +829,6 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
         c->slot = k ^ 1;
         return RT_OK;
     }
-    if (c->pending >= 0) {
-        const int j = c->pending;
-        if (peers) HIP_TRY(hipStreamWaitEvent(st, c->ev_asm[j], 0));
-        HIP_TRY(hipMemcpyAsync(rgb8_dev, c->frame[j], sizeof(uint32_t) * (size_t)c->W * c->H, hipMemcpyDeviceToDevice, st));
-        if (peers) {
-            HIP_TRY(hipEventRecord(c->ev_copy[j], st));
-            c->copied[j] = true;
-        }
-        c->frames += 1;
-        c->pending = -1;
-    }
-    c->slot_deal[k] = c->cur;
     if ((rc = render(c->frame[k], 0)) != RT_OK) return rc;
     if (peers) {
         if (c->copied[k]) HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_copy[k], 0));
@@ -849,6 +838,15 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
         HIP_TRY(hipEventRecord(c->ev_asm[k], c->comm_stream));
     } else if (tv) {
         HIP_TRY(hipEventRecord((*tv)[2], st));
+    }
+    if (j >= 0) {
+        if (peers) HIP_TRY(hipStreamWaitEvent(st, c->ev_asm[j], 0));
+        HIP_TRY(hipMemcpyAsync(rgb8_dev, c->frame[j], sizeof(uint32_t) * (size_t)c->W * c->H, hipMemcpyDeviceToDevice, st));
+        if (peers) {
+            HIP_TRY(hipEventRecord(c->ev_copy[j], st));
+            c->copied[j] = true;
+        }
+        c->frames += 1;
     }
     c->pending = k;
     c->slot = k ^ 1;

@@ -44,6 +44,14 @@ for s in "$@"; do
             step d8_auto 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --ns 8 --deal balanced --out gpurun_out/depth8.jsonl
             step d8_f4 400 env GPU_MAX_HW_QUEUES=8 RT_PS_PIPELINE=1 RT_PS_DEPTH=4 python tools/shard_time.py --scene mig16 --strong --ns 8 --deal balanced --out gpurun_out/depth8.jsonl
             step d8_f6 400 env GPU_MAX_HW_QUEUES=8 RT_PS_PIPELINE=1 RT_PS_DEPTH=6 python tools/shard_time.py --scene mig16 --strong --ns 8 --deal balanced --out gpurun_out/depth8.jsonl ;;
+        primab)    # leaf primitive records: the three float4 loaded together against the AC edge after the type test
+            export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
+            step pab_tp 300 python tools/ab.py variants/prim_eager.so variants/prim_lazy.so --scene teapotF --rounds 9 --frames 60 --check
+            step pab_mig 300 env RT_WAVE_PRIMARY=1 python tools/ab.py variants/prim_eager.so variants/prim_lazy.so --scene mig16 --rounds 9 --frames 30 --check
+            step pab_mig_lane 300 env RT_WAVE_PRIMARY=0 python tools/ab.py variants/prim_eager.so variants/prim_lazy.so --scene mig16 --rounds 7 --frames 30 --check
+            step pab_c3 300 python tools/ab.py variants/prim_eager.so variants/prim_lazy.so --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
+            step pab_c5 300 python tools/ab.py variants/prim_eager.so variants/prim_lazy.so --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
+            unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
         scalarab)  # the wave walk's pairs / leaf records through the scalar cache against vector loads
             export RT_WAVE_PRIMARY=1 RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
             step sab_mig 300 python tools/ab.py variants/walk_scalar.so variants/walk_vector.so --scene mig16 --rounds 9 --frames 30 --check

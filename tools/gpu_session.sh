@@ -61,6 +61,15 @@ for s in "$@"; do
             step prab_c3 300 python tools/ab.py $V --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
             step prab_c5 300 python tools/ab.py $V --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
             unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
+        slabab)    # slab test as three packed pairs (v_pk_add_f32 / v_pk_mul_f32) against six scalar products
+            export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
+            V="variants/slab_pk.so variants/slab_sc.so"
+            step slab_tp 300 python tools/ab.py $V --scene teapotF --rounds 9 --frames 60 --check
+            step slab_mig 300 env RT_WAVE_PRIMARY=1 python tools/ab.py $V --scene mig16 --rounds 9 --frames 30 --check
+            step slab_mig_lane 300 env RT_WAVE_PRIMARY=0 python tools/ab.py $V --scene mig16 --rounds 7 --frames 30 --check
+            step slab_c3 300 python tools/ab.py $V --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
+            step slab_c5 300 python tools/ab.py $V --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
+            unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
         scalarab)  # the wave walk's pairs / leaf records through the scalar cache against vector loads
             export RT_WAVE_PRIMARY=1 RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
             step sab_mig 300 python tools/ab.py variants/walk_scalar.so variants/walk_vector.so --scene mig16 --rounds 9 --frames 30 --check

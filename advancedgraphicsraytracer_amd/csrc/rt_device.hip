@@ -207,6 +207,12 @@ struct rt_renderer {
     // explicit tile deal of rt_render_shard_tiles (FrameArgs::tile_map): local -> global tile,
     // uploaded when it changes; and rank 0's per-global-tile (shard << 24 | local) for assembly
     std::vector<uint32_t> map_host;
+    // the tiles whose running averages the accumulator holds: those of the last frame (a frame
+    // accumulates exactly its own tiles).  0 none yet, 1 every tile, 2 the interleaved shard
+    // held_shard of held_nshards, 3 the explicit list held_list (renderer_held_tiles)
+    int held_kind = 0;
+    uint32_t held_shard = 0, held_nshards = 1;
+    std::vector<uint32_t> held_list;
     uint32_t *d_work = nullptr;     // dry-run work frame: per local tile (work_frame)
     uint32_t work_cap = 0;
     uint32_t *d_map = nullptr;
@@ -1283,6 +1289,14 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     FrameArgs F;
     if (int rc = frame_args(r, cam, p, shard, nshards, tiles, ntiles_map, F); rc != RT_OK) return rc;
     const uint32_t tiles_x = F.tiles_x, tiles_y = (r->H + 7) / 8, ntiles = tiles_x * tiles_y;
+    if (tiles) {
+        r->held_kind = 3;
+        r->held_list = r->map_host;
+    } else {
+        r->held_kind = nshards == 1 ? 1 : 2;
+        r->held_shard = shard;
+        r->held_nshards = nshards;
+    }
     F.packed_out = packed;
     F.out = out;
     F.fwd_src = fwd_src;
@@ -1681,6 +1695,24 @@ int rt::render_work(rt_renderer *r, const rt_camera *cam, const rt_frame_params 
     if (tiles || n)
         return work_frame(r, cam, p, 0, 1, tiles ? tiles : reinterpret_cast<const uint32_t *>(r), n, work, nullptr, (hipStream_t)stream);
     return work_frame(r, cam, p, shard, nshards, nullptr, 0, work, nullptr, (hipStream_t)stream);
+}
+
+bool rt::renderer_held_tiles(const rt_renderer *r, std::vector<uint32_t> &tiles) {
+    tiles.clear();
+    const uint32_t ntiles = ((r->W + 7) / 8) * ((r->H + 7) / 8);
+    switch (r->held_kind) {
+    case 1:
+        for (uint32_t t = 0; t < ntiles; ++t) tiles.push_back(t);
+        return true;
+    case 2:
+        for (uint32_t t = r->held_shard; t < ntiles; t += r->held_nshards) tiles.push_back(t);
+        return true;
+    case 3:
+        tiles = r->held_list;
+        return true;
+    default:
+        return false;
+    }
 }
 
 int rt::renderer_geometry(const rt_renderer *r, uint32_t *W, uint32_t *H, int *device) {

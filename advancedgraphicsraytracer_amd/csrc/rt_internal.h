@@ -45,6 +45,9 @@ int build_sbvh(const rt_prim *prims, const float *transforms, uint32_t n, Bvh &o
 
 // frame size and device of a renderer (rt_multi.cpp)
 int renderer_geometry(const rt_renderer *r, uint32_t *W, uint32_t *H, int *device);
+// the 8x8 tiles whose running averages the renderer's accumulator holds (its last frame's tiles:
+// all of them after a whole frame, a shard's after a shard); false before its first frame
+bool renderer_held_tiles(const rt_renderer *r, std::vector<uint32_t> &tiles);
 // the renderer's device accumulator (W*H float4 = 16 B each); and the accumulator values of
 // the 8x8 tiles listed in DEVICE memory (tiles_dev) packed as [i][64] float4 into buf_dev /
 // written back from it (pixels outside the frame: 0 / skipped), in stream order on `stream`

@@ -178,6 +178,7 @@ struct rt_comm {
     uint32_t *d_status = nullptr;          // accumulator moves: world status words (own at [rank])
     uint32_t *h_status = nullptr;          // ... read back (pinned)
     bool mig_pending = false;              // ev_mig[1] marks a move whose list upload may still run
+    bool adopted = false;                  // the bound renderers' accumulators are on this deal
     uint64_t n_exchanges = 0, n_migrations = 0, n_mig_skipped = 0;
     // RT_MULTI_TIMING: per frame (render start, render end, gather end) events, summed by rt_comm_timing
     std::vector<std::array<hipEvent_t, 3>> tev;
@@ -229,6 +230,7 @@ void free_buffers(rt_comm *c) {
     c->pkey = 0;
     c->pcalls = 0;
     c->settled = false;
+    c->adopted = false;
 }
 
 uint64_t deal_hash(const std::vector<uint32_t> &tiles, const std::vector<uint32_t> &off) {
@@ -535,6 +537,80 @@ int migrate(rt_comm *c, rt_renderer *r, const Deal &from, const Deal &to, hipStr
     return RT_OK;
 }
 
+// The first frame of a communicator on its renderers (a new communicator, or another renderer
+// bound) that does not reset the accumulation: the renderers' accumulators hold the tiles of
+// their last frames -- another communicator's deal, whole frames, or nothing yet -- and not
+// necessarily this communicator's deal (a communicator destroyed and created again
+// around the same renderer).  One exchange of every rank's held tile list; each tile's running
+// average then moves from a rank that holds it (its new owner if that one does, else the lowest
+// rank that does) to its owner under the current deal, through migrate().  Tiles no rank holds
+// stay as they are (fresh renderers: every accumulator starts from zero, as the plain renderer's).
+// Collective failure as in rebalance: the status word travels in the exchange.
+int adopt(rt_comm *c, rt_renderer *r, hipStream_t st) {
+    const Rccl &R = rccl();
+    const uint32_t B = 2 + c->ntiles;       // d_setup holds world blocks of (2 + ntiles) words
+    std::vector<uint32_t> held;
+    const bool known = renderer_held_tiles(r, held);
+    std::vector<uint32_t> block(2 + held.size(), 0u);
+    block[0] = known ? 1u : 0u;
+    block[1] = (uint32_t)held.size();
+    std::copy(held.begin(), held.end(), block.begin() + 2);
+    hipStream_t cs = c->comm_stream;
+    uint32_t *own = c->d_setup + (size_t)c->rank * B;
+    int local = RT_OK;
+    HIP_TRY(hipEventRecord(c->ev_mig[0], st));   // the caller's earlier frames, then the exchange
+    HIP_TRY(hipStreamWaitEvent(cs, c->ev_mig[0], 0));
+    hipError_t up = hipMemcpyAsync(own, block.data(), sizeof(uint32_t) * block.size(), hipMemcpyHostToDevice, cs);
+    if (up != hipSuccess) {
+        local = fail(RT_ERR_HIP, std::string("held tile upload: ") + hipGetErrorString(up));
+        (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(own), 2u, 1, cs);
+    }
+    NCCL_TRY(R, R.group_start(), "ncclGroupStart");
+    for (int q = 0; q < c->world; ++q) {
+        if (q == c->rank) continue;
+        ncclResult_t e = R.send(own, sizeof(uint32_t) * B, ncclUint8, q, c->comm, cs);
+        if (e == ncclSuccess) e = R.recv(c->d_setup + (size_t)q * B, sizeof(uint32_t) * B, ncclUint8, q, c->comm, cs);
+        if (e != ncclSuccess) {
+            (void)R.group_end();
+            return comm_fail(R, e, "held tile exchange");
+        }
+    }
+    NCCL_TRY(R, R.group_end(), "ncclGroupEnd");
+    std::vector<uint32_t> all((size_t)B * c->world);
+    HIP_TRY(hipMemcpyAsync(all.data(), c->d_setup, sizeof(uint32_t) * all.size(), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
+    if (local != RT_OK) return local;
+    // (the own block was written before the copy back: `all` holds it too)
+    std::vector<uint32_t> src(c->ntiles, 0xffffffffu);   // the rank each tile's average comes from
+    const Deal &cur = *c->cur;
+    for (int q = 0; q < c->world; ++q) {
+        const uint32_t *b = all.data() + (size_t)q * B;
+        if (b[0] & 2u) return fail(RT_ERR_COMM, "rt_render_frame_multi: rank " + std::to_string(q) + " failed before the held tile exchange");
+        if (b[1] > c->ntiles) return fail(RT_ERR_COMM, "rt_render_frame_multi: bad held tile list");
+        for (uint32_t i = 0; i < b[1]; ++i) {
+            const uint32_t t = b[2 + i];
+            if (t >= c->ntiles) return fail(RT_ERR_COMM, "rt_render_frame_multi: bad held tile list");
+            if (src[t] == 0xffffffffu || (int)cur.owner[t] == q) src[t] = (uint32_t)q;   // lowest holder, or the owner
+        }
+    }
+    bool moves = false;
+    std::vector<uint32_t> tiles, off(1, 0);
+    for (int q = 0; q < c->world; ++q) {
+        for (uint32_t t = 0; t < c->ntiles; ++t) {
+            const uint32_t from = src[t] == 0xffffffffu ? cur.owner[t] : src[t];
+            if ((int)from != q) continue;
+            tiles.push_back(t);
+            moves = moves || from != cur.owner[t];
+        }
+        off.push_back((uint32_t)tiles.size());
+    }
+    if (!moves) return RT_OK;
+    DealP from;
+    int rc = make_deal(c, std::move(tiles), std::move(off), 0, from);
+    if (rc != RT_OK) return rc;
+    return migrate(c, r, *from, cur, st);
+}
+
 }  // namespace
 
 extern "C" {
@@ -707,6 +783,10 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
     // balanced on measured tile costs -- kept across camera moves; each parameter set tries to
     // rebalance on its kDealAfter-th frame (then 2x, 4x, ... until every rank has costs).  Every
     // rank takes the same decisions: same frames, same parameters, same flags.
+    if (c->world > 1 && !c->adopted) {   // the renderers' accumulators onto this communicator's deal
+        if (!p->reset && (rc = adopt(c, r, st)) != RT_OK) return rc;
+        c->adopted = true;
+    }
     DealP next = c->cur;
     if (c->world > 1) {
         if (!(flags & RT_MULTI_BALANCED)) {

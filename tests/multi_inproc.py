@@ -20,6 +20,10 @@ MODE: sync | pipelined -- the interleaved deal;
       moving   -- balanced, then the camera moves every frame with the accumulator reset (the
                   deal is kept), then a new static camera (rebalanced; the switch frame resets);
       ptbal    -- path-traced frames only (spp 16, depth 10), balanced on the dry-run work map;
+      recreate -- balanced; after 20 frames every rank destroys its communicator and creates a
+                  new one (a second unique id) around the SAME renderer, which must take the new
+                  communicator's deals (a reused communicator address must not revive
+                  the old tile map);
       fault:<site>:<rank> -- balanced, with RT_MULTI_FAULT=<site>:<rank> (csrc/rt_multi.cpp): that
                   rank's local step of a per-frame collective fails; every rank must return an
                   error from the same call and none may be left waiting in the collective.
@@ -38,7 +42,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import advancedgraphicsraytracer_amd as rt  # noqa: E402
 
-BALANCED_MODES = ("balanced", "moving", "ptbal")
+BALANCED_MODES = ("balanced", "moving", "ptbal", "recreate")
 
 
 def plan_for(mode):
@@ -59,6 +63,8 @@ def plan_for(mode):
         return static + moving + settle                              # (the rebalancing one) resets
     if mode == "ptbal":
         return [(16, 10, 0, False)] * 10
+    if mode == "recreate":
+        return [(1, 1, 0, False)] * 40
     if mode.startswith("fault:"):
         return [(1, 1, 0, False)] * 40
     raise SystemExit(f"unknown mode {mode}")
@@ -82,7 +88,10 @@ def camera_for(W, H, shift):
     return cam
 
 
-def rank_main(rank, world, uid, recipe, W, H, mode, plan, results, errors):
+RECREATE_AT = 20
+
+
+def rank_main(rank, world, uid, recipe, W, H, mode, plan, results, errors, uid2=None):
     try:
         L = rt.lib()
         torch.cuda.set_device(0)
@@ -100,6 +109,14 @@ def rank_main(rank, world, uid, recipe, W, H, mode, plan, results, errors):
         failed_at = None
         with torch.cuda.stream(st):
             for f, (spp, depth, shift, reset) in enumerate(plan):
+                if mode == "recreate" and f == RECREATE_AT:   # a new communicator, the same renderer
+                    rt._check(L.rt_multi_flush(r.h, h, optr, C.c_void_p(st.cuda_stream)))
+                    if rank == 0:
+                        copies.append(out.clone())
+                    st.synchronize()
+                    rt._check(L.rt_comm_destroy(h))
+                    h = C.c_void_p()
+                    rt._check(L.rt_comm_create(uid2, rank, world, 0, C.byref(h)))
                 cam = camera_for(W, H, shift)
                 p = r.params(spp, depth, f, reset)
                 rc = L.rt_render_frame_multi(r.h, h, C.byref(cam), C.byref(p), optr, flags, C.c_void_p(st.cuda_stream))
@@ -107,7 +124,7 @@ def rank_main(rank, world, uid, recipe, W, H, mode, plan, results, errors):
                     failed_at = (f, rc, L.rt_last_error().decode(errors="replace"))
                     break
                 rt._check(rc)
-                if rank == 0 and (not pipelined or f > 0):
+                if rank == 0 and (not pipelined or (f > 0 and not (mode == "recreate" and f == RECREATE_AT))):
                     copies.append(out.clone())       # on st: no host sync before the next call
                 b, stats = C.c_int(), (C.c_uint64 * 4)()
                 rt._check(L.rt_comm_deal_info(h, C.byref(b), None, None, stats))
@@ -150,8 +167,10 @@ def main():
     L = rt.lib()
     uid = (C.c_uint8 * rt.RT_COMM_ID_BYTES)()
     rt._check(L.rt_comm_unique_id(uid))
+    uid2 = (C.c_uint8 * rt.RT_COMM_ID_BYTES)()
+    rt._check(L.rt_comm_unique_id(uid2))
     results, errors = [None] * world, []
-    threads = [threading.Thread(target=rank_main, args=(k, world, uid, recipe, W, H, mode, plan, results, errors))
+    threads = [threading.Thread(target=rank_main, args=(k, world, uid, recipe, W, H, mode, plan, results, errors, uid2))
                for k in range(world)]
     for t in threads:
         t.start()
@@ -193,6 +212,9 @@ def main():
             # balancing attempt (which may rebuild the same cut: a valid rebalance either way)
             per, ex = results[0]["deal_per_frame"], results[0]["exchanges_per_frame"]
             deal_ok = deal_ok and per[30:40] == [per[29]] * 10 and ex[30:40] == [ex[29]] * 10 and ex[-1] > ex[39]
+        if mode == "recreate":   # the new communicator starts interleaved and balances again
+            per = results[0]["deal_per_frame"]
+            deal_ok = deal_ok and per[RECREATE_AT - 1] == 1 and per[RECREATE_AT] == 0 and per[-1] == 1
     ok = len(got) == len(plan) and not bad_frames and not bad_acc and all(sums[key] == c[key] for key in sums) and deal_ok
     print(json.dumps({"ok": ok, "world": world, "mode": mode, "frames": len(got), "bad_frames": bad_frames,
                       "bad_acc_ranks": bad_acc, "counters": sums, "want_counters": {k: c[k] for k in sums},

@@ -67,6 +67,13 @@ struct rt_scene {
     bool pt_wavefront = true;   // depth >= 2 path tracing: wavefront (k_pt_level) vs one kernel (k_render)
     uint32_t pt_drain_level = 64;   // bounce level from which the wavefront always drains (64 = never forced)
     double pt_drain_rounds = 0.25;  // ... and it drains any level holding <= this many rounds of resident lanes
+    // small batches (<= pt_small_rounds rounds of resident lanes, e.g. a 1/8 shard's): always drain
+    // from level pt_drain_small (0 = off).  Config 5's 1/8 shard (4.1 M paths per batch, ~10 rounds):
+    // 1.126 / 1.129 -> 1.055 / 1.059 ms forced from level 4 (1.095 / 1.068 from 3); whole frames
+    // (33 M paths, ~84 rounds) lose with it (CFG5-sub 6.70 -> 6.85 ms), so they keep the threshold
+    // alone (profiles/r05/c5drain)
+    uint32_t pt_drain_small = 4;
+    double pt_small_rounds = 16.0;
     bool tile_order = true;         // measured-cost (longest first) tile order (RT_TILE_ORDER=0: off)
     uint32_t split_units = 40000;   // sample split below this many tiles (1080p = 32,400 tiles)
     bool xcd_order = false;         // measured order grouped by XCD: blocks b, b + 8, ... (one XCD) render
@@ -625,6 +632,8 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     // RT_PT_DRAIN_LEVEL / RT_PT_MEM_MB: wavefront drain level and path-state budget (A/B runs)
     if (const char *e = std::getenv("RT_PT_DRAIN_LEVEL")) s->pt_drain_level = (uint32_t)std::max(1, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_DRAIN_ROUNDS")) s->pt_drain_rounds = std::max(0.0, std::atof(e));
+    if (const char *e = std::getenv("RT_PT_DRAIN_SMALL")) s->pt_drain_small = (uint32_t)std::max(0, std::atoi(e));
+    if (const char *e = std::getenv("RT_PT_SMALL_ROUNDS")) s->pt_small_rounds = std::max(0.0, std::atof(e));
     if (const char *e = std::getenv("RT_TILE_ORDER")) s->tile_order = std::atoi(e) != 0;
     // RT_SPLIT_UNITS: sample-split target units (0 = never split)
     if (const char *e = std::getenv("RT_SPLIT_UNITS")) s->split_units = (uint32_t)std::max(0, std::atoi(e));
@@ -907,7 +916,8 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         P.result = pipe ? r->d_res[par] + (size_t)s0 * npix : reinterpret_cast<float4 *>(take(np * 16u));
         P.sum = r->d_sum;
         P.tile_cost = tile_cost;
-        P.drain_level = drain_level;
+        uint32_t dlevel = drain_level;   // this batch's (a small batch drains from pt_drain_small on)
+        P.drain_level = dlevel;
         P.drain_below = 0;
         P.s0 = s0;
         P.batch_spp = std::min<uint32_t>((uint32_t)batch, F.spp - s0);
@@ -926,8 +936,12 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
                 resident = s->ext ? kext::launch_pt_level(view, F, P, tex, lv, s->num_cus, X)
                                   : kcore::launch_pt_level(view, F, P, tex, lv, s->num_cus, X);
             }
-            if (level >= drain_level) break;           // that launch finished every remaining level
-            if (level == 0) P.drain_below = (uint32_t)std::min<double>(4e9, s->pt_drain_rounds * resident);
+            if (level >= dlevel) break;                // that launch finished every remaining level
+            if (level == 0) {
+                P.drain_below = (uint32_t)std::min<double>(4e9, s->pt_drain_rounds * resident);
+                if (s->pt_drain_small && (double)P.npaths <= s->pt_small_rounds * resident)
+                    P.drain_level = dlevel = std::min(dlevel, s->pt_drain_small);
+            }
         }
         if (!pipe) {   // serial: this batch's samples onto the running sum (the last: accumulate, RGB8)
             const bool last = s0 + P.batch_spp >= F.spp;

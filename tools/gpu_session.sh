@@ -92,6 +92,37 @@ for s in "$@"; do
             step c5_slots4 300 env GPU_MAX_HW_QUEUES=8 RT_PT_SLOTS=4 python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/c5hwq.jsonl
             step c5_trace 300 env GPU_MAX_HW_QUEUES=8 rocprofv3 --kernel-trace --stats -d gpurun_out/c5tr -o run --output-format csv -- python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved
             step c5_trsum 60 bash -c "python tools/trace_frames.py gpurun_out/c5tr/run_kernel_trace.csv --tail 0.5 --json gpurun_out/c5tr.json" ;;
+        c5drain)   # config 5's 1/8 shard (last rank, interleaved, 16 queues): forced drain level / drain threshold / slots
+            C5="python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/c5drain.jsonl"
+            step c5d_def 300 env GPU_MAX_HW_QUEUES=16 $C5
+            for lv in 2 3 4 6; do step c5d_lv$lv 300 env GPU_MAX_HW_QUEUES=16 RT_PT_DRAIN_LEVEL=$lv $C5; done
+            step c5d_r1 300 env GPU_MAX_HW_QUEUES=16 RT_PT_DRAIN_ROUNDS=1 $C5
+            step c5d_r0 300 env GPU_MAX_HW_QUEUES=16 RT_PT_DRAIN_ROUNDS=0.0625 $C5
+            step c5d_s4 300 env GPU_MAX_HW_QUEUES=16 RT_PT_SLOTS=4 $C5
+            step c5d_def2 300 env GPU_MAX_HW_QUEUES=16 $C5 ;;
+        c5drain2)  # forced drain level 3 / 4 against the default: the 1/8 shard again (interleaved runs) and whole frames
+            C5="python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 24 --ns 8 --ranks last --deal interleaved --out gpurun_out/c5drain2.jsonl"
+            for rep in 1 2; do
+                for lv in 64 4 3; do step c5d2_lv${lv}_$rep 300 env GPU_MAX_HW_QUEUES=16 RT_PT_DRAIN_LEVEL=$lv $C5; done
+            done
+            for lv in 64 4 3; do
+                step c5d2_b5_lv$lv 300 env RT_PT_DRAIN_LEVEL=$lv python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline
+                step c5d2_b3_lv$lv 300 env RT_PT_DRAIN_LEVEL=$lv python bench.py --config 3 --steps 40 --warmup 5 --no-cpu-baseline
+            done ;;
+        c5small)   # small-batch drain (RT_PT_DRAIN_SMALL=4, default) against none on config 5's 1/2, 1/4, 1/8 shards and whole frames
+            for rep in 1 2; do
+                for ds in 4 0; do
+                    step c5s_ds${ds}_$rep 600 env GPU_MAX_HW_QUEUES=16 RT_PT_DRAIN_SMALL=$ds python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 2,4,8 --ranks last --deal interleaved --out gpurun_out/c5small.jsonl
+                done
+            done
+            for ds in 4 0; do step c5s_b5_ds$ds 300 env RT_PT_DRAIN_SMALL=$ds python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline; done ;;
+        c5small2)  # small-batch drain threshold: 16 rounds (default: the 1/8 shard), 64 (every shard), 0 (off)
+            for rep in 1 2; do
+                for sr in 16 64 0; do
+                    step c5s2_sr${sr}_$rep 600 env GPU_MAX_HW_QUEUES=16 RT_PT_SMALL_ROUNDS=$sr python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 2,4,8 --ranks last --deal interleaved --out gpurun_out/c5small2.jsonl
+                done
+            done
+            for sr in 16 0; do step c5s2_b5_sr$sr 300 env RT_PT_SMALL_ROUNDS=$sr python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline; done ;;
         hwqab)     # interleaved A/B of 8 vs 16 hardware queues on the N > 1 shards and config 5 / 3 at N = 1
             for q in 8 16 8 16; do
                 step ab_c5_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/hwqab.jsonl

@@ -70,6 +70,15 @@ for s in "$@"; do
             step slab_c3 300 python tools/ab.py $V --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
             step slab_c5 300 python tools/ab.py $V --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
             unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
+        divab)     # triangle quotients skipped when the numerator decides the reject, against always dividing
+            export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
+            V="variants/div1.so variants/div0.so"
+            step div_tp 300 python tools/ab.py $V --scene teapotF --rounds 9 --frames 60 --check
+            step div_mig 300 env RT_WAVE_PRIMARY=1 python tools/ab.py $V --scene mig16 --rounds 9 --frames 30 --check
+            step div_mig_lane 300 env RT_WAVE_PRIMARY=0 python tools/ab.py $V --scene mig16 --rounds 7 --frames 30 --check
+            step div_c3 300 python tools/ab.py $V --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
+            step div_c5 300 python tools/ab.py $V --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
+            unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
         topab)     # the stack's top entry in a register (pop without an LDS read first) against the plain LDS stack
             export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
             V="variants/top1.so variants/top0.so"

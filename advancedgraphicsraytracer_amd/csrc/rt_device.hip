@@ -47,6 +47,16 @@ using namespace rt;
                         std::string(#expr) + ": " + hipGetErrorString(e_));                   \
     } while (0)
 
+// RT_PT_QUADS=1: the lane kernel walks two-level node records (build_quads).  Exact (the GPU suite
+// passes with it on; test_wavefront_equals_one_kernel_path_tracer runs it), but measured slower,
+// so off by default (tools/ab.py serial frames, profiles/r05/quadab): CFG3-sub 2.133 -> 2.385 ms,
+// CFG5-sub 8.49 -> 9.41, TEAPOT-F depth 10 1.150 -> 1.253, mig29 x16 spp 4 depth 4 3.78 -> 4.40 --
+// a record step costs four slab tests, two box unions and a 128-B load for every lane of the
+// wave whichever branch (leaf, odd half, record) each lane is in, and the lanes' chains shrink less
+// than the step grows.
+#ifndef RT_PT_QUADS_DEFAULT
+#define RT_PT_QUADS_DEFAULT 0
+#endif
 struct rt_scene {
     int device = 0;
     SceneView view{};
@@ -57,6 +67,8 @@ struct rt_scene {
                                 // plain build, 8 = the single-sample one wherever it applies (RT_FRAME_WAVES)
     uint32_t num_cus = 256;     // CUs of the device (resident grids, frames-in-flight rules)
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
+    bool quads = false;         // two-level node records built (RT_PT_QUADS=1, build_quads); the lane kernel walks them
+    void *d_quads = nullptr;
     bool nested = true;         // every child box lies inside its parent's (as floats): the wave walk's
                                 // exactness needs it (the builders' trees always; a caller's prebuilt one
                                 // is checked at rt_scene_create)
@@ -270,6 +282,73 @@ constexpr int kTuneRestarts = 4;
 #ifndef RT_STACK_ROUND
 #define RT_STACK_ROUND 1u
 #endif
+// Two-level node records (the path tracer's lane kernel, k_pt_lanes<.., true>): one 128-B
+// record per interior node x at even depth (the root at 0) holding the node entries of x's
+// grandchildren -- slots 2h, 2h+1 = the children of x's child h -- or, for a leaf child h, that
+// leaf's own entry in slot 2h (flag bit 0 in its .w word).  One load then serves two binary
+// levels: the walk tests x's children on boxes rebuilt as the union of their children's (the
+// reference's node bounds ARE that union -- each node's box is the min / max over its primitives'
+// bounds, Scene::UpdateNodeBounds, template/scene.h:855-865 -- checked bit for bit here), then
+// the nearer child's children on their own entries, in the reference's order and against the
+// same r.t: the visits are the binary walk's exactly.  A popped odd-depth child is addressed by
+// (its parent's record, half) and reads its children pair from that record.  Entry words: leaf
+// (leftFirst << 8 | count) as in the binary array, even-depth interior node (record << 8), odd
+// marker ((kQuadOdd | record << 1 | half) << 8).  false (no records) when a box is NaN, a parent is
+// not the exact union of its children (a caller's prebuilt tree), or the tree is too large.
+constexpr uint32_t kQuadOdd = 1u << 23;
+bool build_quads(const Bvh &b, std::vector<float4> &rec, uint32_t &root_word) {
+    const Node *N = b.nodes.data();
+    if (b.nodes_used < 3 || N[0].count > 0) return false;
+    std::vector<int32_t> id(b.nodes_used, -1);
+    std::vector<std::pair<uint32_t, uint32_t>> st{{0u, 0u}};
+    std::vector<uint32_t> order;
+    while (!st.empty()) {   // pre-order, even-depth interior nodes numbered as met
+        auto [k, d] = st.back();
+        st.pop_back();
+        const Node &nd = N[k];
+        if (nd.count > 0) continue;
+        if (!(d & 1u)) { id[k] = (int32_t)order.size(); order.push_back(k); }
+        st.push_back({nd.leftFirst + 1, d + 1});
+        st.push_back({nd.leftFirst, d + 1});
+    }
+    if (order.size() >= (kQuadOdd >> 1)) return false;
+    auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
+    // the union of two floats as the device's fminf / fmaxf gives it, or fail on NaN / +-0 ties
+    auto pick = [&](float a, float c, bool mn, float want) {
+        if (a != a || c != c || want != want) return false;
+        if (a == c && bits(a) != bits(c)) return false;
+        const float u = mn ? (a < c ? a : c) : (a > c ? a : c);
+        return bits(u) == bits(want);
+    };
+    auto entry = [&](uint32_t g, float4 *q) {
+        const Node &nd = N[g];
+        const uint32_t w = nd.count > 0 ? ((nd.leftFirst << 8) | nd.count) : ((uint32_t)id[g] << 8);
+        q[0] = make_float4(nd.mn[0], nd.mn[1], nd.mn[2], nd.mx[0]);
+        q[1] = make_float4(nd.mx[1], nd.mx[2], ubits(w), 0.0f);
+    };
+    rec.assign(8 * order.size(), make_float4(0, 0, 0, 0));
+    for (size_t r = 0; r < order.size(); ++r) {
+        const Node &x = N[order[r]];
+        for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t c = x.leftFirst + h;
+            float4 *q = &rec[8 * r + 4 * h];
+            const Node &cn = N[c];
+            if (cn.count > 0) {
+                entry(c, q);
+                q[1].w = ubits(1u);
+                continue;
+            }
+            const Node &g1 = N[cn.leftFirst], &g2 = N[cn.leftFirst + 1];
+            for (int a = 0; a < 3; ++a)
+                if (!pick(g1.mn[a], g2.mn[a], true, cn.mn[a]) || !pick(g1.mx[a], g2.mx[a], false, cn.mx[a])) return false;
+            entry(cn.leftFirst, q);
+            entry(cn.leftFirst + 1, q + 2);
+        }
+    }
+    root_word = (uint32_t)id[0] << 8;
+    return true;
+}
+
 uint32_t pick_stack(uint32_t depth) {   // entries needed <= tree depth (rounded up to RT_STACK_ROUND)
     uint32_t need = depth < 2 ? 2 : depth;
     return (need + RT_STACK_ROUND - 1u) / RT_STACK_ROUND * RT_STACK_ROUND;
@@ -321,7 +400,7 @@ void free_scene(rt_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     (void)hipDeviceSynchronize();
-    void *ptrs[] = {s->d_nodes, s->d_prims, s->d_shade, s->d_mats, s->d_sky, s->d_xprims, s->d_tex, s->d_scratch};
+    void *ptrs[] = {s->d_nodes, s->d_prims, s->d_shade, s->d_mats, s->d_sky, s->d_xprims, s->d_tex, s->d_scratch, s->d_quads};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -443,6 +522,13 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         uint32_t word = (nd.leftFirst << 8) | nd.count;
         nodes[2 * i] = make_float4(nd.mn[0], nd.mn[1], nd.mn[2], nd.mx[0]);
         nodes[2 * i + 1] = make_float4(nd.mx[1], nd.mx[2], ubits(word), 0.0f);
+    }
+    std::vector<float4> quads;
+    uint32_t quad_root = 0;
+    {
+        bool want = RT_PT_QUADS_DEFAULT != 0;
+        if (const char *e = std::getenv("RT_PT_QUADS")) want = std::atoi(e) != 0;
+        s->quads = want && build_quads(s->bvh, quads, quad_root);
     }
     // ---- leaf-order primitive records and per-id shading records; cubes and quads keep
     // their matrices and data in a side table (8 float4 each)
@@ -573,6 +659,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (rc == RT_OK) rc = upload(&s->d_sky, sky);
     if (rc == RT_OK) rc = upload(&s->d_xprims, xprims);
     if (rc == RT_OK) rc = upload(&s->d_tex, texels);
+    if (rc == RT_OK && s->quads) rc = upload(&s->d_quads, quads);
     if (rc == RT_OK && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(RT_ERR_HIP, "hipStreamCreate failed");
     if (rc != RT_OK) { free_scene(s); return rc; }
@@ -585,6 +672,9 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     v.sky = (const uint32_t *)s->d_sky;
     v.xprims = (const float4 *)s->d_xprims;
     v.tex = (const uint32_t *)s->d_tex;
+    v.quads = s->quads ? (const float4 *)s->d_quads : nullptr;
+    v.quad_root = quad_root;
+    v.quad_lanes = 0;
     v.sky_w = sw; v.sky_h = sh;
     v.sky_const = sky_const ? 1 : 0;
     {
@@ -811,6 +901,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
                         (s->walk == RT_WALK_WAVE || (s->walk == RT_WALK_AUTO && r->tune == kTuneDone && r->wave));
     view.walk_stats = r->d_counters;
     view.walk_check = r->walk_check;
+    view.quad_lanes = s->quads ? 1 : 0;
     const uint64_t npix = (uint64_t)F.ntiles_local * 64u;
     // pipelined: per-sample results of the whole frame in a frame-level buffer (two by frame
     // parity, up to 2 GB each); the serial path keeps them per batch with a running sum

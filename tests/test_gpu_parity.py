@@ -515,6 +515,8 @@ def test_frame_kernel_name(rt):
     ("cfg3", 64, 48, 2, 32, {}),                                # the deepest Trace (32): meta bits, records
     ("cfg3", 136, 80, 4, 4, {"RT_PT_LANES": "0"}),              # chunk kernel at every level
     ("teapotF", 200, 120, 1, 10, {"RT_PT_LANES": "0", "RT_PT_DYNAMIC": "0"}),   # static chunks
+    ("cfg3", 136, 80, 4, 4, {"RT_PT_QUADS": "1"}),              # the lane kernel on two-level node records
+    ("cfg5", 96, 64, 3, 10, {"RT_PT_QUADS": "1", "RT_PT_DRAIN_SMALL": "0"}),
 ])
 def test_wavefront_equals_one_kernel_path_tracer(rt, torch, monkeypatch, recipe, W, H, spp, depth, env):
     """The wavefront path tracer (k_pt_level + k_pt_finish: compaction between bounce

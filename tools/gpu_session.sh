@@ -88,6 +88,14 @@ for s in "$@"; do
             step top_c3 300 python tools/ab.py $V --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
             step top_c5 300 python tools/ab.py $V --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
             unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
+        quadab)    # the lane kernel on two-level node records (one 128-B load per two binary levels) against binary pairs
+            export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
+            V="variants/quad1.so variants/quad0.so"
+            step quad_c3 300 python tools/ab.py $V --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
+            step quad_c5 300 python tools/ab.py $V --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
+            step quad_tp10 300 python tools/ab.py $V --scene teapotF --spp 1 --depth 10 --rounds 7 --frames 20 --check
+            step quad_mig4 300 python tools/ab.py $V --scene mig16 --spp 4 --depth 4 --rounds 7 --frames 10 --check
+            unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
         scalarab)  # the wave walk's pairs / leaf records through the scalar cache against vector loads
             export RT_WAVE_PRIMARY=1 RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
             step sab_mig 300 python tools/ab.py variants/walk_scalar.so variants/walk_vector.so --scene mig16 --rounds 9 --frames 30 --check
@@ -217,6 +225,14 @@ for s in "$@"; do
                 step sum_c$c 60 python tools/roofline.py summarize cfg$c "$k" gpurun_out/pc$c/trace gpurun_out/pc$c/fetch gpurun_out/pc$c/write gpurun_out/pc$c/sq gpurun_out/pc$c/tcc $sel --out gpurun_out/pmc_summary.json
             done
             unset RT_PS_PIPELINE RT_PT_PIPELINE ;;
+        mix24)     # instruction mix of the primary+shadow frame kernel, configs 2 and 4 (serial frames, timed launches)
+            export RT_PS_PIPELINE=0
+            for c in 2 4; do
+                b="python bench.py --config $c --steps 60 --warmup 2 --no-cpu-baseline --no-companion --no-strong --ramp-seconds 0.3"
+                step mix_c${c}_a 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES -d gpurun_out/mix$c/a -o pmc --output-format csv -- $b
+                step mix_c${c}_b 300 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY -d gpurun_out/mix$c/b -o pmc --output-format csv -- $b
+            done
+            unset RT_PS_PIPELINE ;;
         prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 100 --warmup 5 --no-cpu-baseline ;;
         listpmc) step listpmc 120 rocprofv3 -L ;;
         pmclds)

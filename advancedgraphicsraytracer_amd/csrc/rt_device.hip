@@ -54,6 +54,14 @@ using namespace rt;
 // a record step costs four slab tests, two box unions and a 128-B load for every lane of the
 // wave whichever branch (leaf, odd half, record) each lane is in, and the lanes' chains shrink less
 // than the step grows.
+// RT_PRIO_FRAC: the leading fraction of the measured tile order runs at raised wave priority
+// (FrameArgs::prio_units).  Measured without effect, so 0 (profiles/r05/prio: config 4's 1/8
+// shard 0.0776 / 0.0765 ms at 0 against 0.0765-0.0791 at 0.03 / 0.1 / 0.3; whole frames 0.2467 /
+// 0.2452 / 0.244 ms; TEAPOT-F 0.0943 / 0.094 / 0.0941): the costliest tiles' steps wait on their
+// loads, not on issue slots.
+#ifndef RT_PRIO_FRAC_DEFAULT
+#define RT_PRIO_FRAC_DEFAULT 0.0
+#endif
 #ifndef RT_PT_QUADS_DEFAULT
 #define RT_PT_QUADS_DEFAULT 0
 #endif
@@ -87,6 +95,7 @@ struct rt_scene {
     uint32_t pt_drain_small = 4;
     double pt_small_rounds = 16.0;
     bool tile_order = true;         // measured-cost (longest first) tile order (RT_TILE_ORDER=0: off)
+    double prio_frac = RT_PRIO_FRAC_DEFAULT;   // leading fraction of that order run at raised wave priority (RT_PRIO_FRAC)
     uint32_t split_units = 40000;   // sample split below this many tiles (1080p = 32,400 tiles)
     bool xcd_order = false;         // measured order grouped by XCD: blocks b, b + 8, ... (one XCD) render
                                     // one compact screen region of 1/8 of the frame's cost (L2 locality)
@@ -725,6 +734,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_PT_DRAIN_SMALL")) s->pt_drain_small = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_SMALL_ROUNDS")) s->pt_small_rounds = std::max(0.0, std::atof(e));
     if (const char *e = std::getenv("RT_TILE_ORDER")) s->tile_order = std::atoi(e) != 0;
+    if (const char *e = std::getenv("RT_PRIO_FRAC")) s->prio_frac = std::max(0.0, std::min(1.0, std::atof(e)));
     // RT_SPLIT_UNITS: sample-split target units (0 = never split)
     if (const char *e = std::getenv("RT_SPLIT_UNITS")) s->split_units = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_FRAME_WAVES")) {
@@ -1262,6 +1272,7 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
             ++r->split_phase;
         }
         F.order = split ? r->d_order + n : r->d_order;
+        F.prio_units = (uint32_t)std::min<double>(F.ntiles_local, r->scene->prio_frac * n);
         F.nunits = F.ntiles_local * F.nchunks + (split ? r->order_split * (r->order_parts - 1u) : 0u);   // split only with nchunks 1
         F.part_shift = r->order_parts == 8 ? 3u : r->order_parts == 4 ? 4u : 5u;
     }

@@ -149,6 +149,32 @@ for s in "$@"; do
                 done
             done
             for sr in 16 0; do step c5s2_b5_sr$sr 300 env RT_PT_SMALL_ROUNDS=$sr python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline; done ;;
+        mig8tr)    # config 4's 1/8 balanced shard (last rank) under a kernel trace: durations, overlap, busy fraction
+            step m8_tr 300 env GPU_MAX_HW_QUEUES=8 rocprofv3 --kernel-trace --stats -d gpurun_out/m8tr -o run --output-format csv -- python tools/shard_time.py --scene mig16 --strong --ns 8 --ranks last --deal balanced --frames 200
+            step m8_trsum 60 python tools/trace_frames.py gpurun_out/m8tr/run_kernel_trace.csv --tail 0.3 --json gpurun_out/m8tr.json ;;
+        fw8)       # config 4's balanced 1/4 and 1/8 shards: the single-sample 8-wave build forced vs the small-frame rule
+            for rep in 1 2; do
+                for fw in 0 8; do
+                    step fw8_${fw}_$rep 400 env GPU_MAX_HW_QUEUES=8 RT_FRAME_WAVES=$fw python tools/shard_time.py --scene mig16 --strong --ns 4,8 --ranks all --deal balanced --out gpurun_out/fw8.jsonl
+                done
+            done ;;
+        deep8)     # config 4's 1/8 balanced shard: frames in flight against hardware queues (8 / 16)
+            M8="python tools/shard_time.py --scene mig16 --strong --ns 8 --ranks last --deal balanced --out gpurun_out/deep8.jsonl"
+            step d8q8 300 env GPU_MAX_HW_QUEUES=8 $M8
+            step d8q16 300 env GPU_MAX_HW_QUEUES=16 $M8
+            step d8q16f6 300 env GPU_MAX_HW_QUEUES=16 RT_PS_PIPELINE=1 RT_PS_DEPTH=6 $M8
+            step d8q16f8 300 env GPU_MAX_HW_QUEUES=16 RT_PS_PIPELINE=1 RT_PS_DEPTH=8 $M8
+            step d8q16f4 300 env GPU_MAX_HW_QUEUES=16 RT_PS_PIPELINE=1 RT_PS_DEPTH=4 $M8
+            step d8q8f8 300 env GPU_MAX_HW_QUEUES=8 RT_PS_PIPELINE=1 RT_PS_DEPTH=8 $M8 ;;
+        prio)      # raised wave priority (s_setprio 3) for the leading fraction of the measured tile order
+            M8="python tools/shard_time.py --scene mig16 --strong --ns 1,8 --ranks last --deal balanced --out gpurun_out/prio.jsonl"
+            for rep in 1 2; do
+                for pf in 0 0.03 0.1 0.3; do step prio_${pf}_$rep 300 env GPU_MAX_HW_QUEUES=8 RT_PRIO_FRAC=$pf $M8; done
+            done
+            for pf in 0 0.03 0.1; do
+                step prio_b4_$pf 300 env RT_PRIO_FRAC=$pf python bench.py --config 4 --steps 200 --warmup 5 --no-cpu-baseline --no-strong
+                step prio_b2_$pf 300 env RT_PRIO_FRAC=$pf python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-strong
+            done ;;
         hwqab)     # interleaved A/B of 8 vs 16 hardware queues on the N > 1 shards and config 5 / 3 at N = 1
             for q in 8 16 8 16; do
                 step ab_c5_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/hwqab.jsonl

@@ -96,6 +96,12 @@ for s in "$@"; do
             step quad_tp10 300 python tools/ab.py $V --scene teapotF --spp 1 --depth 10 --rounds 7 --frames 20 --check
             step quad_mig4 300 python tools/ab.py $V --scene mig16 --spp 4 --depth 4 --rounds 7 --frames 10 --check
             unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
+        ptknob)    # the lane kernel's step budget between shading points and its shading batch
+            export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
+            V="${PTK_V:-variants/base.so variants/b32.so variants/b40.so variants/b48.so variants/b32s48.so}"
+            step ptk_c3 400 python tools/ab.py $V --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
+            step ptk_c5 400 python tools/ab.py $V --scene cfg5 --spp 16 --depth 10 --rounds 5 --frames 6 --check
+            unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
         scalarab)  # the wave walk's pairs / leaf records through the scalar cache against vector loads
             export RT_WAVE_PRIMARY=1 RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
             step sab_mig 300 python tools/ab.py variants/walk_scalar.so variants/walk_vector.so --scene mig16 --rounds 9 --frames 30 --check

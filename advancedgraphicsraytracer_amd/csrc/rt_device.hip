@@ -241,6 +241,7 @@ struct rt_renderer {
     int held_kind = 0;
     uint32_t held_shard = 0, held_nshards = 1;
     std::vector<uint32_t> held_list;
+    uint64_t map_gen = 0, held_gen = 0;   // set_tile_map's changes; the one held_list was copied at
     uint32_t *d_work = nullptr;     // dry-run work frame: per local tile (work_frame)
     uint32_t work_cap = 0;
     uint32_t *d_map = nullptr;
@@ -844,6 +845,7 @@ int set_tile_map(rt_renderer *r, const uint32_t *tiles, uint32_t n, uint32_t nti
     if (n) HIP_TRY(hipMemcpy(r->d_map, tiles, sizeof(uint32_t) * n, hipMemcpyHostToDevice));
     r->map_host.assign(tiles, tiles + n);
     r->map_hash = h;
+    r->map_gen += 1;
     return RT_OK;
 }
 
@@ -1405,9 +1407,12 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
     FrameArgs F;
     if (int rc = frame_args(r, cam, p, shard, nshards, tiles, ntiles_map, F); rc != RT_OK) return rc;
     const uint32_t tiles_x = F.tiles_x, tiles_y = (r->H + 7) / 8, ntiles = tiles_x * tiles_y;
-    if (tiles) {
+    if (tiles) {   // (copied only when the map changed: frames of one deal keep the same list)
+        if (r->held_kind != 3 || r->held_gen != r->map_gen) {
+            r->held_list = r->map_host;
+            r->held_gen = r->map_gen;
+        }
         r->held_kind = 3;
-        r->held_list = r->map_host;
     } else {
         r->held_kind = nshards == 1 ? 1 : 2;
         r->held_shard = shard;

@@ -181,6 +181,13 @@ for s in "$@"; do
                 step prio_b4_$pf 300 env RT_PRIO_FRAC=$pf python bench.py --config 4 --steps 200 --warmup 5 --no-cpu-baseline --no-strong
                 step prio_b2_$pf 300 env RT_PRIO_FRAC=$pf python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-strong
             done ;;
+        ptwalk)    # path-traced configs: level-0 camera rays on the wave walk (forced) against the default lane walk
+            for rep in 1 2; do
+                for w in 0 1; do
+                    step ptw_c3_w${w}_$rep 300 env RT_WAVE_PRIMARY=$w python bench.py --config 3 --steps 40 --warmup 5 --no-cpu-baseline
+                    step ptw_c5_w${w}_$rep 300 env RT_WAVE_PRIMARY=$w python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline
+                done
+            done ;;
         hwqab)     # interleaved A/B of 8 vs 16 hardware queues on the N > 1 shards and config 5 / 3 at N = 1
             for q in 8 16 8 16; do
                 step ab_c5_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/hwqab.jsonl

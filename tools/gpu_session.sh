@@ -102,6 +102,14 @@ for s in "$@"; do
             step ptk_c3 400 python tools/ab.py $V --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
             step ptk_c5 400 python tools/ab.py $V --scene cfg5 --spp 16 --depth 10 --rounds 5 --frames 6 --check
             unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
+        wsab)      # shadow rays on a wave-coherent any-hit walk (with the camera walk) against per-lane IsOccluded
+            export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
+            V="variants/ws1.so variants/ws0.so"
+            step ws_mig 300 env RT_WAVE_PRIMARY=1 python tools/ab.py $V --scene mig16 --rounds 9 --frames 30 --check
+            step ws_mig720 300 env RT_WAVE_PRIMARY=1 python tools/ab.py $V --scene mig16 --w 1280 --h 720 --rounds 9 --frames 40 --check
+            step ws_tp 300 env RT_WAVE_PRIMARY=1 python tools/ab.py $V --scene teapotF --rounds 9 --frames 60 --check
+            step ws_c3 300 env RT_WAVE_PRIMARY=1 python tools/ab.py $V --scene cfg3 --spp 1 --depth 1 --rounds 9 --frames 30 --check
+            unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
         scalarab)  # the wave walk's pairs / leaf records through the scalar cache against vector loads
             export RT_WAVE_PRIMARY=1 RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
             step sab_mig 300 python tools/ab.py variants/walk_scalar.so variants/walk_vector.so --scene mig16 --rounds 9 --frames 30 --check

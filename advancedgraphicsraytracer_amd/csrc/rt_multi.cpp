@@ -557,22 +557,24 @@ int adopt(rt_comm *c, rt_renderer *r, hipStream_t st) {
     std::copy(held.begin(), held.end(), block.begin() + 2);
     hipStream_t cs = c->comm_stream;
     uint32_t *own = c->d_setup + (size_t)c->rank * B;
+    // local steps before the group collect their error: the rank still enters the group (with
+    // status bit 2) so that no peer is left waiting in it
+    hipError_t e = hipEventRecord(c->ev_mig[0], st);   // the caller's earlier frames, then the exchange
+    if (e == hipSuccess) e = hipStreamWaitEvent(cs, c->ev_mig[0], 0);
+    if (e == hipSuccess) e = hipMemcpyAsync(own, block.data(), sizeof(uint32_t) * block.size(), hipMemcpyHostToDevice, cs);
     int local = RT_OK;
-    HIP_TRY(hipEventRecord(c->ev_mig[0], st));   // the caller's earlier frames, then the exchange
-    HIP_TRY(hipStreamWaitEvent(cs, c->ev_mig[0], 0));
-    hipError_t up = hipMemcpyAsync(own, block.data(), sizeof(uint32_t) * block.size(), hipMemcpyHostToDevice, cs);
-    if (up != hipSuccess) {
-        local = fail(RT_ERR_HIP, std::string("held tile upload: ") + hipGetErrorString(up));
+    if (e != hipSuccess) {
+        local = fail(RT_ERR_HIP, std::string("held tile upload: ") + hipGetErrorString(e));
         (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(own), 2u, 1, cs);
     }
     NCCL_TRY(R, R.group_start(), "ncclGroupStart");
     for (int q = 0; q < c->world; ++q) {
         if (q == c->rank) continue;
-        ncclResult_t e = R.send(own, sizeof(uint32_t) * B, ncclUint8, q, c->comm, cs);
-        if (e == ncclSuccess) e = R.recv(c->d_setup + (size_t)q * B, sizeof(uint32_t) * B, ncclUint8, q, c->comm, cs);
-        if (e != ncclSuccess) {
+        ncclResult_t ne = R.send(own, sizeof(uint32_t) * B, ncclUint8, q, c->comm, cs);
+        if (ne == ncclSuccess) ne = R.recv(c->d_setup + (size_t)q * B, sizeof(uint32_t) * B, ncclUint8, q, c->comm, cs);
+        if (ne != ncclSuccess) {
             (void)R.group_end();
-            return comm_fail(R, e, "held tile exchange");
+            return comm_fail(R, ne, "held tile exchange");
         }
     }
     NCCL_TRY(R, R.group_end(), "ncclGroupEnd");

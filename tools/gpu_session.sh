@@ -196,6 +196,18 @@ for s in "$@"; do
                     step ptw_c5_w${w}_$rep 300 env RT_WAVE_PRIMARY=$w python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline
                 done
             done ;;
+        mig8pmc)   # config 4's 1/8 balanced shard (last rank): wave wait / VALU / L2 counters of its frame kernel
+            M8="python tools/shard_time.py --scene mig16 --strong --ns 8 --ranks last --deal balanced --frames 200"
+            step m8_sq 300 env GPU_MAX_HW_QUEUES=8 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d gpurun_out/m8pmc/sq -o pmc --output-format csv -- $M8
+            step m8_tcc 300 env GPU_MAX_HW_QUEUES=8 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/m8pmc/tcc -o pmc --output-format csv -- $M8 ;;
+        finprio)   # overlapped frames' finishing passes on a high-priority stream (RT_FIN_PRIO=1) against the caller's stream
+            for rep in 1 2; do
+                for fp in 0 1; do
+                    step fp_m_${fp}_$rep 300 env GPU_MAX_HW_QUEUES=8 RT_FIN_PRIO=$fp python tools/shard_time.py --scene mig16 --strong --ns 1,4,8 --ranks last --deal balanced --out gpurun_out/finprio.jsonl
+                    step fp_t_${fp}_$rep 300 env GPU_MAX_HW_QUEUES=8 RT_FIN_PRIO=$fp python tools/shard_time.py --scene teapotF --w 1280 --h 720 --ns 1,8 --ranks last --deal interleaved --out gpurun_out/finprio.jsonl
+                    step fp_c5_${fp}_$rep 300 env GPU_MAX_HW_QUEUES=16 RT_FIN_PRIO=$fp python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/finprio.jsonl
+                done
+            done ;;
         hwqab)     # interleaved A/B of 8 vs 16 hardware queues on the N > 1 shards and config 5 / 3 at N = 1
             for q in 8 16 8 16; do
                 step ab_c5_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/hwqab.jsonl

@@ -59,6 +59,11 @@ using namespace rt;
 // shard 0.0776 / 0.0765 ms at 0 against 0.0765-0.0791 at 0.03 / 0.1 / 0.3; whole frames 0.2467 /
 // 0.2452 / 0.244 ms; TEAPOT-F 0.0943 / 0.094 / 0.0941): the costliest tiles' steps wait on their
 // loads, not on issue slots.
+// RT_FIN_PRIO=1 (off): overlapped frames' finishing passes on a high-priority stream.  Measured
+// far slower (profiles/r05/finprio: config 4's 1/8 shard 0.077 -> 0.236-0.244 ms, whole frames
+// 0.241-0.245 -> 0.290-0.293, TEAPOT-F 720p 1/8 0.052-0.056 -> 0.078, config 5's 1/8 shard even):
+// the two extra cross-stream hops per frame cost more than the queueing they avoid, and the
+// timed frames-in-flight choice falls back to 1-2 in flight.
 #ifndef RT_FIN_PRIO_DEFAULT
 #define RT_FIN_PRIO_DEFAULT 0
 #endif

@@ -71,8 +71,6 @@ struct FrameArgs {
     const uint32_t *order;              // tile dispatch order: local tile of slot i (nullptr = identity); an
                                         // entry with bit 31 renders part (bits 28-30) of its tile only
     uint32_t part_shift;                // lanes per part of a split tile = 1 << part_shift (5: halves)
-    uint32_t prio_units;                // the first prio_units dispatch slots (the costliest tiles of the
-                                        // measured order) raise their wave's issue priority (s_setprio)
     uint32_t *tile_cost;                // if set: each tile's wave cycles (to build the order)
     float4 *acc;
     uint32_t *out;

@@ -54,22 +54,6 @@ using namespace rt;
 // a record step costs four slab tests, two box unions and a 128-B load for every lane of the
 // wave whichever branch (leaf, odd half, record) each lane is in, and the lanes' chains shrink less
 // than the step grows.
-// RT_PRIO_FRAC: the leading fraction of the measured tile order runs at raised wave priority
-// (FrameArgs::prio_units).  Measured without effect, so 0 (profiles/r05/prio: config 4's 1/8
-// shard 0.0776 / 0.0765 ms at 0 against 0.0765-0.0791 at 0.03 / 0.1 / 0.3; whole frames 0.2467 /
-// 0.2452 / 0.244 ms; TEAPOT-F 0.0943 / 0.094 / 0.0941): the costliest tiles' steps wait on their
-// loads, not on issue slots.
-// RT_FIN_PRIO=1 (off): overlapped frames' finishing passes on a high-priority stream.  Measured
-// far slower (profiles/r05/finprio: config 4's 1/8 shard 0.077 -> 0.236-0.244 ms, whole frames
-// 0.241-0.245 -> 0.290-0.293, TEAPOT-F 720p 1/8 0.052-0.056 -> 0.078, config 5's 1/8 shard even):
-// the two extra cross-stream hops per frame cost more than the queueing they avoid, and the
-// timed frames-in-flight choice falls back to 1-2 in flight.
-#ifndef RT_FIN_PRIO_DEFAULT
-#define RT_FIN_PRIO_DEFAULT 0
-#endif
-#ifndef RT_PRIO_FRAC_DEFAULT
-#define RT_PRIO_FRAC_DEFAULT 0.0
-#endif
 #ifndef RT_PT_QUADS_DEFAULT
 #define RT_PT_QUADS_DEFAULT 0
 #endif
@@ -103,8 +87,6 @@ struct rt_scene {
     uint32_t pt_drain_small = 4;
     double pt_small_rounds = 16.0;
     bool tile_order = true;         // measured-cost (longest first) tile order (RT_TILE_ORDER=0: off)
-    bool fin_prio = RT_FIN_PRIO_DEFAULT != 0;   // overlapped frames' finishing passes on a high-priority stream (RT_FIN_PRIO)
-    double prio_frac = RT_PRIO_FRAC_DEFAULT;   // leading fraction of that order run at raised wave priority (RT_PRIO_FRAC)
     uint32_t split_units = 40000;   // sample split below this many tiles (1080p = 32,400 tiles)
     bool xcd_order = false;         // measured order grouped by XCD: blocks b, b + 8, ... (one XCD) render
                                     // one compact screen region of 1/8 of the frame's cost (L2 locality)
@@ -221,10 +203,6 @@ struct rt_renderer {
     uint32_t ps_prev = 0;           // frames in flight of the previous eligible frame (0 serial)
     hipEvent_t pev[16] = {};
     hipEvent_t ps_join = nullptr;   // caller's stream -> overlap stream, on a switch to overlapped
-    // RT_FIN_PRIO: overlapped frames' finishing passes on a high-priority stream (fin_stream),
-    // behind the caller's stream (fin_in) and ahead of it again (fin_out)
-    hipStream_t fin_stream = nullptr;
-    hipEvent_t fin_in = nullptr, fin_out = nullptr;
     hipEvent_t cost_ev = nullptr;   // path-traced frames: the cost map was cleared (caller's stream)
     float ps_ms[8] = {};
     // the overlapped frames' per-sample results, frame n in buffer n % buffers (kernel on
@@ -748,8 +726,6 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_PT_DRAIN_SMALL")) s->pt_drain_small = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_SMALL_ROUNDS")) s->pt_small_rounds = std::max(0.0, std::atof(e));
     if (const char *e = std::getenv("RT_TILE_ORDER")) s->tile_order = std::atoi(e) != 0;
-    if (const char *e = std::getenv("RT_FIN_PRIO")) s->fin_prio = std::atoi(e) != 0;
-    if (const char *e = std::getenv("RT_PRIO_FRAC")) s->prio_frac = std::max(0.0, std::min(1.0, std::atof(e)));
     // RT_SPLIT_UNITS: sample-split target units (0 = never split)
     if (const char *e = std::getenv("RT_SPLIT_UNITS")) s->split_units = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_FRAME_WAVES")) {
@@ -885,26 +861,6 @@ int ensure_pipe_streams(rt_renderer *r, int n) {
         HIP_TRY(hipEventCreateWithFlags(&r->pt_lv[k], hipEventDisableTiming | hipEventReleaseToDevice));
         r->nstreams = k + 1;
     }
-    return RT_OK;
-}
-
-// RT_FIN_PRIO: where an overlapped frame's finishing pass runs -- a high-priority stream, so that
-// its few workgroups are not queued behind the frames' long render waves.  It follows everything
-// the caller's stream holds (the frame's kernels included, joined there), and the caller's stream
-// follows it (the launcher records fin_out after the pass): the caller's stream order is kept.
-int fin_stream_for(rt_renderer *r, hipStream_t st, hipStream_t &fst) {
-    fst = st;
-    if (!r->scene->fin_prio) return RT_OK;
-    if (!r->fin_stream) {
-        int lo = 0, hi = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIP_TRY(hipStreamCreateWithPriority(&r->fin_stream, hipStreamNonBlocking, hi));
-        HIP_TRY(hipEventCreateWithFlags(&r->fin_in, hipEventDisableTiming | hipEventReleaseToDevice));
-        HIP_TRY(hipEventCreateWithFlags(&r->fin_out, hipEventDisableTiming | hipEventReleaseToDevice));
-    }
-    HIP_TRY(hipEventRecord(r->fin_in, st));
-    HIP_TRY(hipStreamWaitEvent(r->fin_stream, r->fin_in, 0));
-    fst = r->fin_stream;
     return RT_OK;
 }
 
@@ -1099,14 +1055,8 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
         P.sum = r->d_sum;
         P.s0 = 0;
         P.batch_spp = F.spp;
-        hipStream_t fst = st;
-        if (int rc = fin_stream_for(r, st, fst); rc != RT_OK) return rc;   // RT_FIN_PRIO: a high-priority stream
-        if (s->ext) kext::launch_pt_finish(F, P, true, fst);
-        else kcore::launch_pt_finish(F, P, true, fst);
-        if (fst != st) {
-            HIP_TRY(hipEventRecord(r->fin_out, fst));
-            HIP_TRY(hipStreamWaitEvent(st, r->fin_out, 0));
-        }
+        if (s->ext) kext::launch_pt_finish(F, P, true, st);
+        else kcore::launch_pt_finish(F, P, true, st);
         HIP_TRY(hipEventRecord(r->pt_fin[par], st));
         r->pt_fin_set[par] = true;
     }
@@ -1314,7 +1264,6 @@ int tile_order_step(rt_renderer *r, FrameArgs &F, uint64_t key, int walk_phase, 
             ++r->split_phase;
         }
         F.order = split ? r->d_order + n : r->d_order;
-        F.prio_units = (uint32_t)std::min<double>(F.ntiles_local, r->scene->prio_frac * n);
         F.nunits = F.ntiles_local * F.nchunks + (split ? r->order_split * (r->order_parts - 1u) : 0u);   // split only with nchunks 1
         F.part_shift = r->order_parts == 8 ? 3u : r->order_parts == 4 ? 4u : 5u;
     }
@@ -1774,16 +1723,9 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         PathArgs P{};
         P.batch_spp = p->spp;
         P.result = F.samples;
-        hipStream_t fst = st;
-        if (ps_pipe)
-            if (int rc = fin_stream_for(r, st, fst); rc != RT_OK) return rc;
-        if (s->ext) kext::launch_pt_finish(F, P, true, fst);
-        else kcore::launch_pt_finish(F, P, true, fst);
+        if (s->ext) kext::launch_pt_finish(F, P, true, st);
+        else kcore::launch_pt_finish(F, P, true, st);
         HIP_TRY(hipGetLastError());
-        if (fst != st) {
-            HIP_TRY(hipEventRecord(r->fin_out, fst));
-            HIP_TRY(hipStreamWaitEvent(st, r->fin_out, 0));
-        }
         if (ps_pipe) {
             HIP_TRY(hipEventRecord(r->ps_fin[buf], st));
             r->ps_fin_set[buf] = true;
@@ -2145,9 +2087,6 @@ int rt_renderer_destroy(rt_renderer *r) {
     for (auto &e : r->gate_ev)
         if (e) (void)hipEventDestroy(e);
     if (r->ps_join) (void)hipEventDestroy(r->ps_join);
-    if (r->fin_stream) (void)hipStreamDestroy(r->fin_stream);
-    if (r->fin_in) (void)hipEventDestroy(r->fin_in);
-    if (r->fin_out) (void)hipEventDestroy(r->fin_out);
     if (r->cost_ev) (void)hipEventDestroy(r->cost_ev);
     if (r->stall_ev) (void)hipEventDestroy(r->stall_ev);
     for (int b = 0; b < kPsMaxDepth + 1; ++b) {

@@ -20,6 +20,8 @@ MODE: sync | pipelined -- the interleaved deal;
       moving   -- balanced, then the camera moves every frame with the accumulator reset (the
                   deal is kept), then a new static camera (rebalanced; the switch frame resets);
       ptbal    -- path-traced frames only (spp 16, depth 10), balanced on the dry-run work map;
+      after_tick -- every rank's renderer first renders the first 5 frames whole (Tick), then the
+                  communicator takes over (balanced): each rank holds every tile, nothing moves;
       recreate -- balanced; after 20 frames every rank destroys its communicator and creates a
                   new one (a second unique id) around the SAME renderer, which must take the new
                   communicator's deals (a reused communicator address must not revive
@@ -42,7 +44,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import advancedgraphicsraytracer_amd as rt  # noqa: E402
 
-BALANCED_MODES = ("balanced", "moving", "ptbal", "recreate")
+BALANCED_MODES = ("balanced", "moving", "ptbal", "recreate", "after_tick")
 
 
 def plan_for(mode):
@@ -63,7 +65,7 @@ def plan_for(mode):
         return static + moving + settle                              # (the rebalancing one) resets
     if mode == "ptbal":
         return [(16, 10, 0, False)] * 10
-    if mode == "recreate":
+    if mode in ("recreate", "after_tick"):
         return [(1, 1, 0, False)] * 40
     if mode.startswith("fault:"):
         return [(1, 1, 0, False)] * 40
@@ -89,6 +91,7 @@ def camera_for(W, H, shift):
 
 
 RECREATE_AT = 20
+TICK_FRAMES = 5
 
 
 def rank_main(rank, world, uid, recipe, W, H, mode, plan, results, errors, uid2=None):
@@ -107,8 +110,19 @@ def rank_main(rank, world, uid, recipe, W, H, mode, plan, results, errors, uid2=
         flags = (rt.MULTI_PIPELINED if pipelined else 0) | (rt.MULTI_BALANCED if mode in BALANCED_MODES or fault else 0)
         copies, deals, exch = [], [], []
         failed_at = None
+        first = 0
+        if mode == "after_tick":   # whole frames first, on this rank's own renderer
+            first = TICK_FRAMES
+            for f in range(first):
+                spp, depth, shift, reset = plan[f]
+                r.camera = camera_for(W, H, shift)
+                frame = r.tick_host(spp=spp, depth=depth, frame=f, reset=reset)
+                if rank == 0:
+                    copies.append(torch.from_numpy(frame.view(np.int32).copy()))
         with torch.cuda.stream(st):
             for f, (spp, depth, shift, reset) in enumerate(plan):
+                if f < first:
+                    continue
                 if mode == "recreate" and f == RECREATE_AT:   # a new communicator, the same renderer
                     rt._check(L.rt_multi_flush(r.h, h, optr, C.c_void_p(st.cuda_stream)))
                     if rank == 0:
@@ -124,7 +138,7 @@ def rank_main(rank, world, uid, recipe, W, H, mode, plan, results, errors, uid2=
                     failed_at = (f, rc, L.rt_last_error().decode(errors="replace"))
                     break
                 rt._check(rc)
-                if rank == 0 and (not pipelined or (f > 0 and not (mode == "recreate" and f == RECREATE_AT))):
+                if rank == 0 and (not pipelined or (f > first and not (mode == "recreate" and f == RECREATE_AT))):
                     copies.append(out.clone())       # on st: no host sync before the next call
                 b, stats = C.c_int(), (C.c_uint64 * 4)()
                 rt._check(L.rt_comm_deal_info(h, C.byref(b), None, None, stats))
@@ -197,7 +211,16 @@ def main():
         px = tile_pixels(W, H, results[k]["tiles"])
         if not np.array_equal(results[k]["acc"][px].view(np.uint32), acc[px].view(np.uint32)):
             bad_acc.append(k)
-    c = ref.counters()
+    c = dict(ref.counters())
+    if mode == "after_tick":   # every rank also traced the whole-frame Ticks: world - 1 more copies of them
+        pre = rt.Renderer(rt.Scene.recipe(recipe), W, H)
+        for f in range(TICK_FRAMES):
+            spp, depth, shift, reset = plan[f]
+            pre.camera = camera_for(W, H, shift)
+            pre.tick_host(spp=spp, depth=depth, frame=f, reset=reset)
+        cp = pre.counters()
+        for key in ("primary", "shadow", "bounce"):
+            c[key] += (world - 1) * cp[key]
     sums = {key: sum(results[k]["counters"][key] for k in range(world)) for key in ("primary", "shadow", "bounce")}
     deal = results[0]["deal"]
     deal_ok = True
@@ -212,6 +235,8 @@ def main():
             # balancing attempt (which may rebuild the same cut: a valid rebalance either way)
             per, ex = results[0]["deal_per_frame"], results[0]["exchanges_per_frame"]
             deal_ok = deal_ok and per[30:40] == [per[29]] * 10 and ex[30:40] == [ex[29]] * 10 and ex[-1] > ex[39]
+        if mode == "after_tick":   # every rank held every tile: the first frame moved nothing
+            deal_ok = deal_ok and deal["moves"] == deal["deals_built"]
         if mode == "recreate":   # the new communicator starts interleaved and balances again
             per = results[0]["deal_per_frame"]
             deal_ok = deal_ok and per[RECREATE_AT - 1] == 1 and per[RECREATE_AT] == 0 and per[-1] == 1

@@ -36,6 +36,7 @@ def test_standin_library_exports_the_rccl_subset():
     (2, "balanced", "teapotF", 200, 120), (3, "balanced", "mig16", 256, 144), (1, "balanced", "cfg3", 136, 80),
     (3, "moving", "teapotF", 200, 120),                # camera moves every frame: the deal is kept
     (2, "recreate", "teapotF", 200, 120),              # a new communicator around the same renderer
+    (3, "after_tick", "mig16", 200, 120),              # renderers that accumulated whole frames first
     (8, "pipelined", "teapotF", 1920, 1080),           # the driver's default N = 8 run (weak config 2 deal)
     (8, "balanced", "mig16", 1920, 1080),              # config 4 at N = 8: balanced + pipelined, two switches
     (8, "ptbal", "cfg5", 480, 270),                    # config 5's scene at N = 8: path-traced balanced deal

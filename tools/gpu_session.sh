@@ -214,6 +214,12 @@ for s in "$@"; do
                     step c5ds_${ds}_$rep 300 env GPU_MAX_HW_QUEUES=16 RT_PT_DRAIN_SMALL=$ds python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 24 --ns 8 --ranks last --deal interleaved --out gpurun_out/c5ds.jsonl
                 done
             done ;;
+        c5knobs)   # config 5's 1/8 shard with the small-batch drain: drain threshold and slots, interleaved x3
+            for rep in 1 2 3; do
+                for v in "RT_PT_DRAIN_ROUNDS=0.25" "RT_PT_DRAIN_ROUNDS=0.5" "RT_PT_DRAIN_ROUNDS=0.125" "RT_PT_SLOTS=6"; do
+                    step c5k_${v}_$rep 300 env GPU_MAX_HW_QUEUES=16 $v python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 24 --ns 8 --ranks last --deal interleaved --out gpurun_out/c5knobs.jsonl
+                done
+            done ;;
         hwqab)     # interleaved A/B of 8 vs 16 hardware queues on the N > 1 shards and config 5 / 3 at N = 1
             for q in 8 16 8 16; do
                 step ab_c5_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/hwqab.jsonl

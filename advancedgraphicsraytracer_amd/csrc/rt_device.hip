@@ -86,6 +86,10 @@ struct rt_scene {
     // alone (profiles/r05/c5drain)
     uint32_t pt_drain_small = 4;
     double pt_small_rounds = 16.0;
+    // ... and drains any of its levels holding <= this many rounds (the whole frames' 0.25 above):
+    // the 1/8 shard 1.084 / 1.077 -> 1.054 / 1.065 ms mean of three interleaved runs (0.0625: 1.058;
+    // 0.5: 1.092; profiles/r05/c5drain/c5knobs*.jsonl)
+    double pt_small_drain_rounds = 0.125;
     bool tile_order = true;         // measured-cost (longest first) tile order (RT_TILE_ORDER=0: off)
     uint32_t split_units = 40000;   // sample split below this many tiles (1080p = 32,400 tiles)
     bool xcd_order = false;         // measured order grouped by XCD: blocks b, b + 8, ... (one XCD) render
@@ -725,6 +729,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (const char *e = std::getenv("RT_PT_DRAIN_ROUNDS")) s->pt_drain_rounds = std::max(0.0, std::atof(e));
     if (const char *e = std::getenv("RT_PT_DRAIN_SMALL")) s->pt_drain_small = (uint32_t)std::max(0, std::atoi(e));
     if (const char *e = std::getenv("RT_PT_SMALL_ROUNDS")) s->pt_small_rounds = std::max(0.0, std::atof(e));
+    if (const char *e = std::getenv("RT_PT_SMALL_DRAIN_ROUNDS")) s->pt_small_drain_rounds = std::max(0.0, std::atof(e));
     if (const char *e = std::getenv("RT_TILE_ORDER")) s->tile_order = std::atoi(e) != 0;
     // RT_SPLIT_UNITS: sample-split target units (0 = never split)
     if (const char *e = std::getenv("RT_SPLIT_UNITS")) s->split_units = (uint32_t)std::max(0, std::atoi(e));
@@ -1031,9 +1036,9 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
             }
             if (level >= dlevel) break;                // that launch finished every remaining level
             if (level == 0) {
-                P.drain_below = (uint32_t)std::min<double>(4e9, s->pt_drain_rounds * resident);
-                if (s->pt_drain_small && (double)P.npaths <= s->pt_small_rounds * resident)
-                    P.drain_level = dlevel = std::min(dlevel, s->pt_drain_small);
+                const bool small = s->pt_drain_small && (double)P.npaths <= s->pt_small_rounds * resident;
+                P.drain_below = (uint32_t)std::min<double>(4e9, (small ? s->pt_small_drain_rounds : s->pt_drain_rounds) * resident);
+                if (small) P.drain_level = dlevel = std::min(dlevel, s->pt_drain_small);
             }
         }
         if (!pipe) {   // serial: this batch's samples onto the running sum (the last: accumulate, RGB8)

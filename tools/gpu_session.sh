@@ -216,10 +216,18 @@ for s in "$@"; do
             done ;;
         c5knobs)   # config 5's 1/8 shard with the small-batch drain: drain threshold and slots, interleaved x3
             for rep in 1 2 3; do
-                for v in "RT_PT_DRAIN_ROUNDS=0.25" "RT_PT_DRAIN_ROUNDS=0.5" "RT_PT_DRAIN_ROUNDS=0.125" "RT_PT_SLOTS=6"; do
+                for v in ${C5K_V:-"RT_PT_DRAIN_ROUNDS=0.25" "RT_PT_DRAIN_ROUNDS=0.5" "RT_PT_DRAIN_ROUNDS=0.125" "RT_PT_SLOTS=6"}; do
                     step c5k_${v}_$rep 300 env GPU_MAX_HW_QUEUES=16 $v python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 24 --ns 8 --ranks last --deal interleaved --out gpurun_out/c5knobs.jsonl
                 done
             done ;;
+        c5final)   # config 5's 1/8 shard with the small-batch defaults (drain from 4, threshold 0.125) against the previous 0.25, x3; whole frames
+            for rep in 1 2 3; do
+                for sr in 0.125 0.25; do
+                    step c5f_${sr}_$rep 300 env GPU_MAX_HW_QUEUES=16 RT_PT_SMALL_DRAIN_ROUNDS=$sr python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 24 --ns 8 --ranks last --deal interleaved --out gpurun_out/c5final.jsonl
+                done
+            done
+            step c5f_b5 300 python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline
+            step c5f_b3 300 python bench.py --config 3 --steps 40 --warmup 5 --no-cpu-baseline ;;
         hwqab)     # interleaved A/B of 8 vs 16 hardware queues on the N > 1 shards and config 5 / 3 at N = 1
             for q in 8 16 8 16; do
                 step ab_c5_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/hwqab.jsonl

@@ -228,6 +228,15 @@ for s in "$@"; do
             done
             step c5f_b5 300 python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline
             step c5f_b3 300 python bench.py --config 3 --steps 40 --warmup 5 --no-cpu-baseline ;;
+        c3knobs)   # whole-frame path tracing (configs 3 and 5): drain threshold / level and slots, interleaved x2
+            for rep in 1 2; do
+                for v in "RT_PT_DRAIN_ROUNDS=0.25" "RT_PT_DRAIN_ROUNDS=0.125" "RT_PT_DRAIN_ROUNDS=0.5" "RT_PT_DRAIN_LEVEL=3" "RT_PT_DRAIN_LEVEL=2" "RT_PT_SLOTS=6"; do
+                    step c3k_${v}_$rep 300 env $v python bench.py --config 3 --steps 40 --warmup 5 --no-cpu-baseline
+                done
+                for v in "RT_PT_DRAIN_ROUNDS=0.25" "RT_PT_DRAIN_ROUNDS=0.125"; do
+                    step w5k_${v}_$rep 300 env $v python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline
+                done
+            done ;;
         hwqab)     # interleaved A/B of 8 vs 16 hardware queues on the N > 1 shards and config 5 / 3 at N = 1
             for q in 8 16 8 16; do
                 step ab_c5_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/hwqab.jsonl

@@ -1632,12 +1632,19 @@ int launch_render(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p
         if (r->ps_phase > 0 && r->ps_phase == NG * G) {
             HIP_TRY(hipEventSynchronize(r->pev[2 * NG - 1]));
             for (int g = 0; g < NG; ++g) HIP_TRY(hipEventElapsedTime(&r->ps_ms[g], r->pev[2 * g], r->pev[2 * g + 1]));
-            // group g and its mirror NG - 1 - g ran the same depth; a depth replaces the
-            // shallower one chosen so far (serial first) only when it beats it by kTuneMargin
-            // (tuned_alternative), so noise does not buy frames in flight
-            float best = r->ps_ms[0] + r->ps_ms[NG - 1];
-            r->ps_use = depths[0];
-            for (int g = 1; g < NG / 2; ++g) {
+            // group g and its mirror NG - 1 - g ran the same depth.  Shallow candidates (serial,
+            // 2): 2 in flight replaces serial only when it beats it by kTuneMargin, so noise does not
+            // buy frames in flight.  Deep candidates (tail-bound or small frames: serial, 2, 4, 6):
+            // 4 in flight is the default, which another depth replaces only when it beats it by
+            // kTuneMargin -- the deep groups time a deeper pipeline's gain short (mig29 x16: 4 in
+            // flight 1.9 % ahead of 2 in its groups, 3.5 % ahead in steady state, 0.236-0.238
+            // against 0.246 ms; profiles/r05/c4depth), so with serial as the default the choice
+            // between 2 and 4 was a coin toss
+            const int pref = NG == 8 ? 2 : 0;
+            float best = r->ps_ms[pref] + r->ps_ms[NG - 1 - pref];
+            r->ps_use = depths[pref];
+            for (int g = 0; g < NG / 2; ++g) {
+                if (g == pref) continue;
                 const float t = r->ps_ms[g] + r->ps_ms[NG - 1 - g];
                 if (t < best * (1.0f - kTuneMargin)) { best = t; r->ps_use = depths[g]; }
             }

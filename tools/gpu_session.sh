@@ -237,6 +237,20 @@ for s in "$@"; do
                     step w5k_${v}_$rep 300 env $v python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline
                 done
             done ;;
+        c4depth)   # config 4 whole frame: frames in flight forced 2 / 4 / 6 against the timed choice, interleaved x2
+            for rep in 1 2; do
+                for v in "RT_PS_PIPELINE=-1" "RT_PS_PIPELINE=1 RT_PS_DEPTH=2" "RT_PS_PIPELINE=1 RT_PS_DEPTH=4" "RT_PS_PIPELINE=1 RT_PS_DEPTH=6"; do
+                    n=$(echo $v | tr ' =' '__')
+                    step c4d_${n}_$rep 300 env $v python bench.py --config 4 --steps 200 --warmup 5 --no-cpu-baseline --no-strong
+                done
+            done ;;
+        c4auto)    # the frames-in-flight choice with half the margin between overlapped depths: config 4 (x3), mig29 x16 and TEAPOT-F at 720p
+            for rep in 1 2 3; do
+                step c4a_$rep 300 python bench.py --config 4 --steps 200 --warmup 5 --no-cpu-baseline --no-strong
+            done
+            step c4a_tp 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-strong
+            step c4a_sh8 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --ns 2,4,8 --ranks all --deal balanced --out gpurun_out/c4a_shards.jsonl
+            step c4a_tp8 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene teapotF --ns 8 --ranks last --deal interleaved --out gpurun_out/c4a_shards.jsonl ;;
         hwqab)     # interleaved A/B of 8 vs 16 hardware queues on the N > 1 shards and config 5 / 3 at N = 1
             for q in 8 16 8 16; do
                 step ab_c5_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/hwqab.jsonl

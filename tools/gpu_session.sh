@@ -251,6 +251,11 @@ for s in "$@"; do
             step c4a_tp 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-strong
             step c4a_sh8 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene mig16 --strong --ns 2,4,8 --ranks all --deal balanced --out gpurun_out/c4a_shards.jsonl
             step c4a_tp8 300 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene teapotF --ns 8 --ranks last --deal interleaved --out gpurun_out/c4a_shards.jsonl ;;
+        weak2)     # config 2 as the driver's N > 1 runs it: a 1/N shard at spp N (N = 2, 4, 8), interleaved deal, 8 queues
+            step w2_a 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene teapotF --strong --spp 8 --ns 8 --ranks last --deal interleaved --out gpurun_out/weak2.jsonl
+            step w2_b 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene teapotF --strong --spp 4 --ns 4 --ranks last --deal interleaved --out gpurun_out/weak2.jsonl
+            step w2_c 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene teapotF --strong --spp 2 --ns 2 --ranks last --deal interleaved --out gpurun_out/weak2.jsonl
+            step w2_d 400 env GPU_MAX_HW_QUEUES=8 python tools/shard_time.py --scene teapotF --strong --spp 8 --ns 8 --ranks last --deal interleaved --out gpurun_out/weak2.jsonl ;;
         hwqab)     # interleaved A/B of 8 vs 16 hardware queues on the N > 1 shards and config 5 / 3 at N = 1
             for q in 8 16 8 16; do
                 step ab_c5_q$q 300 env GPU_MAX_HW_QUEUES=$q python tools/shard_time.py --scene cfg5 --depth 10 --spp 16 --strong --warm 8 --frames 16 --ns 8 --ranks last --deal interleaved --out gpurun_out/hwqab.jsonl

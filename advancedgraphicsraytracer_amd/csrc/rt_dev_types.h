@@ -57,6 +57,12 @@ struct SceneView {
 // across the 8 XCDs -- one counter address cost 26 % of the primary+shadow frame.
 constexpr uint32_t kCounterSlots = 1024;
 
+// Launches size their dynamic LDS to at most 64 KB per workgroup (gfx950 allows 160 KB, but every
+// launch here is sized for several workgroups per CU); the dry-run work map keeps 8 per-lane
+// counters past the stacks.
+constexpr size_t kLdsLaunchMax = 65536;
+constexpr size_t kWorkCounterBytes = 8u * 256u * sizeof(uint32_t);
+
 struct FrameArgs {
     float cam_pos[3], cam_tl[3], cam_tr[3], cam_bl[3];
     float lens, rw, rh;

@@ -69,6 +69,7 @@ struct rt_scene {
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
     bool quads = false;         // two-level node records built (RT_PT_QUADS=1, build_quads); the lane kernel walks them
     void *d_quads = nullptr;
+    bool walk_fits = true;      // the lane stacks + the wave walk's word stack fit one launch's LDS (kLdsLaunchMax)
     bool nested = true;         // every child box lies inside its parent's (as floats): the wave walk's
                                 // exactness needs it (the builders' trees always; a caller's prebuilt one
                                 // is checked at rt_scene_create)
@@ -519,6 +520,8 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (s->bvh.max_leaf > 255) { delete s; return fail(RT_ERR_UNSUPPORTED, "BVH leaf with more than 255 primitives"); }
     if (s->bvh.depth > 64) { delete s; return fail(RT_ERR_UNSUPPORTED, "BVH deeper than 64 (the reference's stack[64])"); }
     s->stack_depth = pick_stack(s->bvh.depth);
+    // trees deeper than 60: the lane stacks (depth x 1 KB) leave no room for the walk's words
+    s->walk_fits = (size_t)s->stack_depth * (256u + 4u) * sizeof(uint32_t) <= kLdsLaunchMax;
 
     // ---- device node array: packed (leftFirst << 8 | count) word in b.z
     std::vector<float4> nodes(2 * (size_t)s->bvh.nodes_used);
@@ -769,7 +772,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     }
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
     v.wave_primary = 0;
-    const bool wave_ok = !s->has_cubes && s->nested;
+    const bool wave_ok = !s->has_cubes && s->nested && s->walk_fits;
     s->walk = wave_ok ? RT_WALK_AUTO : RT_WALK_LANE;
     if (const char *e = std::getenv("RT_WAVE_PRIMARY")) s->walk = std::atoi(e) != 0 && wave_ok ? RT_WALK_WAVE : RT_WALK_LANE;
     v.bounds_finite = 1;
@@ -904,7 +907,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
     rt_scene *s = r->scene;
     // camera rays of level 0 take the wave-coherent walk when the scene forces it, or when
     // the renderer's primary+shadow frames timed it faster (RT_WALK_AUTO)
-    view.wave_primary = !s->has_cubes && s->nested &&
+    view.wave_primary = !s->has_cubes && s->nested && s->walk_fits &&
                         (s->walk == RT_WALK_WAVE || (s->walk == RT_WALK_AUTO && r->tune == kTuneDone && r->wave));
     view.walk_stats = r->d_counters;
     view.walk_check = r->walk_check;
@@ -1362,6 +1365,10 @@ int work_frame(rt_renderer *r, const rt_camera *cam, const rt_frame_params *p, u
     if (!r || !cam || !p) return fail(RT_ERR_INVALID, "work frame: null argument");
     if (p->mode != RT_MODE_PATH) return fail(RT_ERR_UNSUPPORTED, "work frame: RT_MODE_PATH frames only");
     if (p->depth > 32) return fail(RT_ERR_UNSUPPORTED, "Trace depth above 32");
+    // the counting build keeps 8 per-lane counters past the stacks (launch_work): a tree deeper than
+    // 56 leaves no room -- UNSUPPORTED, so rebalance() falls back to the measured cycle costs
+    if (stack_bytes(r->scene) + kWorkCounterBytes > kLdsLaunchMax)
+        return fail(RT_ERR_UNSUPPORTED, "work frame: this tree's stacks leave no LDS for the counters");
     FrameArgs F;
     int rc = frame_args(r, cam, p, shard, nshards, tiles, ntiles_map, F);
     if (rc != RT_OK) return rc;
@@ -1911,6 +1918,8 @@ int rt_scene_set_camera_walk(rt_scene *s, int walk) {
         return fail(RT_ERR_UNSUPPORTED, "the wave walk needs order-independent hits; cubes accept on tmax (Primitive.h:221-233)");
     if (walk != RT_WALK_LANE && !s->nested)
         return fail(RT_ERR_UNSUPPORTED, "the wave walk needs every child box inside its parent's (this prebuilt BVH has one outside)");
+    if (walk != RT_WALK_LANE && !s->walk_fits)
+        return fail(RT_ERR_UNSUPPORTED, "the wave walk's word stack does not fit beside this tree's lane stacks (64 KB of LDS)");
     s->walk = walk;
     return RT_OK;
 }

@@ -806,7 +806,13 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
             }
             if (!c->settled && c->pcalls == c->next_try) {
                 bool complete = false;
-                if ((rc = rebalance(c, r, cam, p, next, complete)) != RT_OK) return rc;
+                if ((rc = rebalance(c, r, cam, p, next, complete)) != RT_OK) {
+                    // failed on every rank alike (the status words): the parameter set settles on
+                    // the deal in use instead of retrying a failure every later frame
+                    c->settled = true;
+                    c->pcalls += 1;
+                    return rc;
+                }
                 if (complete) c->settled = true;
                 else c->next_try = c->next_try < (1u << 30) ? 2u * c->next_try : c->next_try;
             }

@@ -25,6 +25,108 @@ import sys
 import time
 
 
+def _gpus_arg(argv):
+    """--gpus N from the command line (any prefix argparse would accept: --gpu, --gp), else 1."""
+    n = 1
+    for i, a in enumerate(argv):
+        key, eq, val = a.partition("=")
+        if len(key) >= 4 and "--gpus".startswith(key):
+            n = int(val if eq else (argv[i + 1] if i + 1 < len(argv) else "1"))
+    return n
+
+
+def launch_plan(argv, env):
+    """How many rank processes bench.py must start itself, decided before anything loads HIP.
+
+    A launcher (python -m torch.distributed.run, or any that exports WORLD_SIZE) owns the ranks: 0.
+    `python bench.py --gpus N` with N > 1 and no WORLD_SIZE: N -- the parent then only spawns N
+    child processes of this script with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set and never
+    touches the GPU itself; silently rendering on one GPU under `--gpus N` would report N = 1 as N."""
+    if env.get("WORLD_SIZE"):
+        return 0
+    n = _gpus_arg(argv)
+    if n < 1:
+        raise SystemExit(f"bench: --gpus {n}: need at least one GPU")
+    return n if n > 1 else 0
+
+
+def _die_with_parent():   # child side of fork, before exec: SIGKILL when the launcher dies
+    try:
+        import ctypes
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, 9)   # PR_SET_PDEATHSIG, SIGKILL
+    except OSError:
+        pass
+
+
+def spawn_ranks(n, argv, script=None, poll_s=0.2):
+    """Run N rank processes of `script` (this file) on 127.0.0.1 and wait for all of them.  Their
+    stdout / stderr are this process's (rank 0 prints the one JSON line).  The first rank to fail
+    ends the others (its own PID only) and its status becomes the launcher's exit status; SIGTERM /
+    SIGINT to the launcher are passed on."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    script = script or os.path.abspath(__file__)
+    procs = []
+
+    def stop_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+        t_end = time.time() + 20
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    def on_signal(sig, _frame):
+        stop_all(sig)
+        sys.exit(128 + sig)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RT_BENCH_LAUNCHER="bench.py")
+            procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env,
+                                          preexec_fn=_die_with_parent))
+        status = 0
+        while [p.poll() for p in procs].count(None):   # poll every rank (any() would stop at the first live one)
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                status = bad[0]
+                print(f"bench: a rank exited with status {status}; stopping the other ranks", file=sys.stderr, flush=True)
+                stop_all()
+                break
+            time.sleep(poll_s)
+        if status == 0:
+            status = next((p.returncode for p in procs if p.returncode), 0)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    return 128 - status if status < 0 else status   # killed by signal k: 128 + k, as a shell reports it
+
+
+if __name__ == "__main__":
+    _n_spawn = launch_plan(sys.argv[1:], os.environ)
+    if _n_spawn:
+        sys.exit(spawn_ranks(_n_spawn, sys.argv[1:]))
+    if os.environ.get("RT_BENCH_LAUNCH_CHECK"):   # tests/test_bench_launch.py: the rank's view, no GPU
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                          "MASTER_PORT", "RT_BENCH_LAUNCHER")}), flush=True)
+        _mode = os.environ["RT_BENCH_LAUNCH_CHECK"].partition(":")
+        if _mode[0] == "fail":   # "fail:R": rank R exits 3, the others wait as if in a collective
+            if os.environ.get("RANK") == _mode[2]:
+                sys.exit(3)
+            time.sleep(600)
+        sys.exit(0)
+
+
 def _queues_wanted(argv, world):
     """Hardware queues this command line (--config / --depth) wants, before anything loads HIP:
     16 for config 5 split over N > 1 ranks, 8 for path tracing (trace depth > 1), config 4 and any
@@ -39,8 +141,8 @@ def _queues_wanted(argv, world):
         elif key == "--depth":
             depth = int(val)
     pt = (depth if depth is not None else {3: 4, 5: 10}.get(cfg, 1)) > 1
-    if cfg == 5 and pt and world > 1:
-        return 16
+    if world > 1 and (cfg == 5 and pt or cfg == 2 and depth in (None, 1)):
+        return 16   # config 5 split over the ranks: the default config-2 run times it too (config5)
     return 8 if (pt or cfg == 4 or world > 1) else None
 
 
@@ -117,7 +219,9 @@ def parse():
     ap.add_argument("--no-companion", action="store_true", help="skip the 1280x720 companion run (profiling runs: "
                     "its frames would share the frame kernel's name in the kernel trace)")
     ap.add_argument("--per-step-events", action="store_true", help="HIP event pair around every launch at N = 1 too")
-    ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling config-4 line (strong_config4) "
+    ap.add_argument("--extra-configs", default="4,3,5", help="BASELINE configs timed after a default config-2 "
+                    "headline in the same process (EXTRA_CONFIGS: strong_config4, config3, config5)")
+    ap.add_argument("--no-strong", action="store_true", help="skip every extra config line (strong_config4, config3, config5) "
                     "that default config-2 runs add after the headline")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the all-cores CPU baseline sample")
     ap.add_argument("--summary", default=rl.SUMMARY, help="rocprofv3 PMC / kernel-trace summary (tools/roofline.py)")
@@ -220,52 +324,69 @@ def companion_rate(scene, W, H, spp, depth, stream, device, warm_s=0.4, frames=3
             "mrays_s": round(rays / wall / 1e6, 3), "fps": round(frames / wall, 3)}
 
 
-def strong_config4(world, rank, device, dist, stream, frames=200, warm_s=1.5, max_warm_s=12.0):
-    """north_star's strong-scaling case beside the default weak line: BASELINE.json config 4
-    (mig29 x16, 1920x1080, 1 spp, primary + shadow) as ONE frame split over the N ranks with the
-    cost-balanced deal (RT_MULTI_BALANCED through rt_render_frame_multi, pipelined), in the same
-    process after the headline loop -- so every --gpus N run also measures the tile-scaling curve.
-    Warm-up: blocks of frames until warm_s seconds have passed AND every rank renders under the
-    balanced deal (N > 1; the renderer's timed choices re-run on the new deal's tiles), agreed
-    over the ranks like the headline's clock ramp.  Then `frames` frames timed between a barrier +
-    synchronize on both sides, max over ranks; then an untimed instrumented pass for every rank's
-    render / exposed-gather split.  At N = 1 the same frames through Renderer.Tick."""
+# The other BASELINE.json GPU configs, timed after the headline in the same process (default
+# config-2 runs): name, scene, spp per GPU, Trace depth, N > 1 scaling, balanced deal, timed frames
+EXTRA_CONFIGS = {
+    4: dict(key="strong_config4", scene="mig16", spp=1, depth=1, scaling="strong", balanced=True, frames=200),
+    3: dict(key="config3", scene="cfg3", spp=4, depth=4, scaling="weak", balanced=False, frames=100),
+    5: dict(key="config5", scene="cfg5", spp=16, depth=10, scaling="strong", balanced=False, frames=30),
+}
+
+
+def extra_config(cfg_no, world, rank, device, dist, stream, summary, warm_s=1.5, max_warm_s=12.0):
+    """One more BASELINE.json config (EXTRA_CONFIGS) beside the default headline, in the same process
+    after it, so the driver's own runs time every GPU config: config 4 (mig29 x16, 1080p, 1 spp,
+    primary + shadow) is north_star's strong-scaling case -- ONE frame split over the N ranks with the
+    cost-balanced deal (RT_MULTI_BALANCED); config 3 (CFG3-sub, 4 spp, depth 4) is weak (each rank a
+    1/N shard at spp 4N, interleaved deal); config 5 (CFG5-sub, 16 spp, depth 10) is strong (one
+    frame split, interleaved deal: the bounce levels' cost is not the camera rays').  All go
+    through rt_render_frame_multi (pipelined) at N > 1 and through Tick at N = 1.
+    Warm-up: blocks of frames until warm_s seconds have passed (and, for config 4 at N > 1, every
+    rank renders under the balanced deal; the renderer's timed choices re-run on the new deal's
+    tiles), agreed over the ranks.  Then `frames` frames timed between a barrier + synchronize on
+    both sides, max over ranks; then an untimed instrumented pass for every rank's render /
+    exposed-gather split.  The roofline row is the config's dominant kernel from the tracked PMC
+    summary (serial frames)."""
     from advancedgraphicsraytracer_amd.distributed import NativeShardedFrame
-    W, H = 1920, 1080
+    ec = EXTRA_CONFIGS[cfg_no]
+    W, H, depth = 1920, 1080, ec["depth"]
+    spp = ec["spp"] * world if ec["scaling"] == "weak" else ec["spp"]
+    frames = ec["frames"]
     dev = f"cuda:{device}"
-    sc = rt.Scene.recipe("mig16", device=device)
-    r4 = rt.Renderer(sc, W, H)
+    sc = rt.Scene.recipe(ec["scene"], device=device)
+    rx = rt.Renderer(sc, W, H)
     out = torch.zeros(W * H, dtype=torch.int32, device=dev)
     sptr = stream.cuda_stream
-    sf = NativeShardedFrame(r4, device=torch.device("cuda", device), balanced=True) if world > 1 else None
+    sf = NativeShardedFrame(rx, device=torch.device("cuda", device), balanced=ec["balanced"]) if world > 1 else None
 
     def step(i):
         with torch.cuda.stream(stream):
             if sf is not None:
-                sf.submit(spp=1, depth=1, frame=i, stream=sptr)
+                sf.submit(spp=spp, depth=depth, frame=i, stream=sptr)
             else:
-                r4.Tick(out, spp=1, depth=1, frame=i, stream=sptr)
+                rx.Tick(out, spp=spp, depth=depth, frame=i, stream=sptr)
 
     def drain():
         if sf is not None:
             with torch.cuda.stream(stream):
                 sf.flush(stream=sptr)
 
+    block = 100 if depth == 1 else 8   # long blocks: the renderer's timed groups (up to 32 frames) fit between syncs
     nf, t0 = 0, time.perf_counter()
     while True:
-        for _ in range(100):   # long blocks: the renderer's timed groups (up to 32 frames) fit between syncs
+        for _ in range(block):
             step(nf)
             nf += 1
         drain()
         torch.cuda.synchronize(device)
         el = time.perf_counter() - t0
-        ready = el >= warm_s and (sf is None or sf.deal_info()["balanced"] == 1)
+        ready = el >= warm_s and (sf is None or not ec["balanced"] or sf.deal_info()["balanced"] == 1)
         go = torch.tensor([1 if (ready or el > max_warm_s) else 0], device=dev)
         if dist:
             dist.all_reduce(go, op=dist.ReduceOp.MIN)
         if go.item():
             break
-    c0 = r4.counters()
+    c0 = rx.counters()
     if dist:
         dist.barrier()
     torch.cuda.synchronize(device)
@@ -277,13 +398,18 @@ def strong_config4(world, rank, device, dist, stream, frames=200, warm_s=1.5, ma
     if dist:
         dist.barrier()
     wall = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
-    c1 = r4.counters()
-    rays = torch.tensor([sum(c1[k] - c0[k] for k in ("primary", "shadow", "bounce"))], dtype=torch.float64, device=dev)
-    res = {"workload": "config 4: mig16 1920x1080, spp 1, Trace depth 1 (primary + NEE shadow), one frame split "
-                       "over the ranks (strong)", "frames": frames, "warm_frames": nf}
+    c1 = rx.counters()
+    per = [c1[k] - c0[k] for k in ("primary", "shadow", "bounce")]
+    rays = torch.tensor([sum(per)] + per, dtype=torch.float64, device=dev)
+    kind = "primary + NEE shadow" if depth == 1 else "path tracing"
+    split = ("one frame split over the ranks (strong)" if ec["scaling"] == "strong"
+             else "each rank a 1/N shard at spp N x %d (weak)" % ec["spp"])
+    res = {"workload": f"config {cfg_no}: {ec['scene']} {W}x{H}, spp {spp}, Trace depth {depth} ({kind}), {split}",
+           "scene": ec["scene"], "spp": spp, "depth": depth, "scaling": ec["scaling"], "frames": frames,
+           "warm_frames": nf}
     if sf is not None:
         sf.set_timing(True)
-        for k in range(20):
+        for k in range(min(frames, 20)):
             step(nf + frames + k)
         drain()
         torch.cuda.synchronize(device)
@@ -294,17 +420,30 @@ def strong_config4(world, rank, device, dist, stream, frames=200, warm_s=1.5, ma
         dist.all_reduce(rays, op=dist.ReduceOp.SUM)
         dist.all_reduce(wall, op=dist.ReduceOp.MAX)
         di = sf.deal_info()
-        res.update(path="rt_render_frame_multi (pipelined, RT_MULTI_BALANCED)",
+        res.update(path="rt_render_frame_multi (pipelined, %s)" % ("RT_MULTI_BALANCED" if ec["balanced"] else "interleaved deal"),
                    deal_rank0={"in_use": "balanced" if di["balanced"] else "interleaved", **di},
                    render_ms_per_frame_by_rank=[round(e[0].item(), 4) for e in every],
-                   gather_ms_per_frame_by_rank=[round(e[1].item(), 4) for e in every])
+                   # rank 0's gather is its receives on the communicator's stream behind its own render:
+                   # the exposed part is not separable from the render there, so it is not reported
+                   gather_ms_per_frame_by_rank=[None] + [round(e[1].item(), 4) for e in every[1:]])
         sf.close()
     else:
-        res.update(path="Renderer.Tick", in_flight=r4.overlap_depth()[0], timed_choices=r4.choices())
+        res.update(path="Renderer.Tick", in_flight=rx.overlap_depth()[0])
+        if depth == 1:
+            res["timed_choices"] = rx.choices()
     w = wall.item()
+    tot, prim, shad, bnc = rays.tolist()
     res.update(ms_per_frame=round(w / frames * 1e3, 4), fps=round(frames / w, 3),
-               rays_per_frame=round(rays.item() / frames), mrays_s=round(rays.item() / w / 1e6, 3))
-    r4.close()
+               rays_per_frame=round(tot / frames), rays={"primary": int(prim), "shadow": int(shad), "bounce": int(bnc)},
+               mrays_s=round(tot / w / 1e6, 3),
+               msamples_per_s=round(W * H * spp / (w / frames) / 1e6, 3),
+               hip_hw_queues=os.environ.get("GPU_MAX_HW_QUEUES", "4 (HIP default)"))
+    key = f"cfg{cfg_no}"
+    if key in summary:   # serial frames' dominant kernel, from the tracked PMC passes
+        roof = rl.roofline(summary[key])
+        roof["source"] = f"profiles/pmc_summary.json[{key}] (tools/roofline.py, serial frames)"
+        res["roofline"] = roof
+    rx.close()
     sc.close()
     return res
 
@@ -314,13 +453,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        args.gpus = world if world > 1 else args.gpus
+    if world != args.gpus:   # never report one GPU's frames as N GPUs' (or the reverse)
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s) (WORLD_SIZE); "
+                         "run `python bench.py --gpus N` alone or under torch.distributed.run --nproc-per-node N")
     dist = None
+    backend = os.environ.get("RT_DIST_BACKEND", "nccl")
     # one rank per GPU; RT_DIST_BACKEND=gloo + fewer GPUs than ranks rehearses the N > 1 path
     # on a single card (ranks share it; the exchange goes through gloo instead of RCCL)
-    device = local % max(1, torch.cuda.device_count()) if world > 1 else 0
-    backend = os.environ.get("RT_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if world > 1 and backend == "nccl" and ndev < world:
+        raise SystemExit(f"bench: {world} ranks over RCCL need {world} GPUs, {ndev} visible "
+                         "(RT_DIST_BACKEND=gloo rehearses N ranks sharing fewer GPUs)")
+    device = local % max(1, ndev) if world > 1 else 0
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -499,17 +643,24 @@ def main():
         walk_check = {"frames": 10, "rays_walked": w1["walked"], "lanes_retraced": w1["retraced"],
                       "margin_boxes": w1["margin_boxes"], "verify_frames": 10,
                       "verify_rays": w2["walked"] - w1["walked"], "verify_mismatch": w2["verify_mismatch"]}
-    strong4 = None
+    extras = {}
     default_cfg2 = (args.config, args.scene, W, H, args.spp, args.depth) == (2, "teapotF", 1920, 1080, 1, 1)
-    if default_cfg2 and not args.no_strong and (world == 1 or sharded is not None and native_fallback is None
-                                                  and backend == "nccl"):
+    extra_list = [int(c) for c in args.extra_configs.split(",") if c.strip()] if not args.no_strong else []
+    if default_cfg2 and extra_list and (world == 1 or sharded is not None and native_fallback is None
+                                        and backend == "nccl"):
         if sharded is not None:   # the headline communicator is done (its frames are flushed)
             sharded.close()
             sharded = None
         # the headline renderer is done too: its streams would share hardware queues with the
-        # config-4 renderer's frames in flight (see the companion below)
+        # next renderer's frames in flight (see the companion below)
         rend.close()
-        strong4 = strong_config4(world, rank, device, dist, stream)
+        summary_x = rl.load(args.summary)
+        for c in extra_list:
+            ec = extra_config(c, world, rank, device, dist, stream, summary_x)
+            extras[EXTRA_CONFIGS[c]["key"]] = ec
+            if rank == 0:
+                print(f"bench: config {c}: {ec['ms_per_frame']} ms per frame, {ec['mrays_s']} Mrays/s",
+                      file=sys.stderr, flush=True)
     companion = None
     if world == 1 and args.depth == 1 and (W, H) == (1920, 1080) and not args.no_companion:   # the metric's other frame size
         # the measured renderer is done: free its streams first, so that the companion's
@@ -556,6 +707,8 @@ def main():
                                    + ", accumulate + RGB8",
                        "scene": args.scene, "width": W, "height": H, "spp": spp, "depth": args.depth,
                        "parallelism": f"screen-tile x{world}" if world > 1 else "single GPU",
+                       "launcher": ("bench.py (spawned the ranks itself)" if os.environ.get("RT_BENCH_LAUNCHER")
+                                    else "external (WORLD_SIZE from the launcher)" if world > 1 else "single process"),
                        "hip_hw_queues": {"effective": os.environ.get("GPU_MAX_HW_QUEUES", "4 (HIP default)"),
                                          "set_by_bench": os.environ.get("GPU_MAX_HW_QUEUES") != _HWQ_BEFORE
                                          or _HWQ_ARG is not None, "environment_before": _HWQ_BEFORE}},
@@ -581,8 +734,7 @@ def main():
             line["multi_gpu"] = multi
         if companion:
             line["at_720p"] = companion
-        if strong4:
-            line["strong_config4"] = strong4
+        line.update(extras)   # strong_config4, config3, config5 (EXTRA_CONFIGS)
         if world == 1 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(args, spp)

@@ -128,3 +128,46 @@ def kat_rays():
     D /= np.linalg.norm(D, axis=1, keepdims=True).astype(np.float32)
     cloud = np.concatenate([O, D.astype(np.float32), np.full((n, 1), 1e34, np.float32)], 1).astype(np.float32)
     return np.concatenate([rays, cloud], 0)
+
+
+def chain_scene(rt, n_tris=60):
+    """A caterpillar tree one primitive per level: the light (prim 0) and n_tris small
+    diffuse triangles in front of the default camera, with a prebuilt BVH whose every interior node
+    has a leaf child and an interior child -- depth n_tris + 1 (61 by default), so the LDS stacks
+    fill 64 KB (64 entries x 256 lanes x 4 B) and leave no room for the wave walk's words or the work
+    map's counters.  Boxes are the unions of their primitives' boxes (nested).  Returns prims,
+    materials, (nodes [n, 32] uint8, indices)."""
+    mats = [rt.material(rt.LIGHT, (24, 24, 22)), rt.material(rt.DIFFUSE, (0.8, 0.7, 0.6)),
+            rt.material(rt.MIRROR, (0.9, 0.9, 0.9))]
+    prims = [rt.sphere((0.0, 4.0, -2.0), 0.5, 0)]
+    boxes = [(np.float32([-0.5, 3.5, -2.5]), np.float32([0.5, 4.5, -1.5]))]
+    cols = 10
+    for k in range(n_tris):
+        x0 = -3.0 + 0.6 * (k % cols)
+        y0 = -1.8 + 0.6 * (k // cols)
+        z = 2.5 + 0.01 * k
+        a, b, c = (x0, y0, z), (x0 + 0.5, y0 + 0.05, z + 0.1), (x0 + 0.1, y0 + 0.5, z - 0.1)
+        prims.append(rt.triangle(a, b, c, 1 + (k % 7 == 3)))
+        v = np.float32([a, b, c])
+        boxes.append((v.min(axis=0), v.max(axis=0)))
+    P = len(prims)
+    nodes = np.zeros((2 * P, 8), np.uint32)
+    f = nodes.view(np.float32)
+
+    def put(i, lo, hi, left_first, count):
+        f[i, 0:3], f[i, 3:6] = lo, hi
+        nodes[i, 6], nodes[i, 7] = left_first, count
+
+    def union(j):   # primitives j .. P-1
+        lo = np.min([boxes[q][0] for q in range(j, P)], axis=0)
+        hi = np.max([boxes[q][1] for q in range(j, P)], axis=0)
+        return lo, hi
+
+    put(0, *union(0), 2, 0)
+    for j in range(P - 1):   # pair (2 + 2j, 3 + 2j): leaf of prim j, then the rest of the chain
+        put(2 + 2 * j, *boxes[j], j, 1)
+        if j == P - 2:
+            put(3 + 2 * j, *boxes[P - 1], P - 1, 1)
+        else:
+            put(3 + 2 * j, *union(j + 1), 4 + 2 * j, 0)
+    return prims, mats, (nodes.view(np.uint8).reshape(len(nodes), 32), np.arange(P, dtype=np.uint32))

@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-from scenes_util import oracle_scene
+from scenes_util import chain_scene, oracle_scene
 
 pytestmark = pytest.mark.gpu
 
@@ -343,6 +343,39 @@ def test_wave_walk_needs_nested_boxes(rt, oracle, scenes, torch):
         want, _ = o.tick(W, H, acc, spp=1, depth=1, frame=fr)
     assert np.array_equal(got, want)
     r.close()
+
+
+def test_deep_prebuilt_tree_keeps_to_64kb_of_lds(rt, oracle, torch):
+    """a prebuilt tree 61 levels deep (tests/scenes_util.chain_scene) fills the 64 KB of
+    lane stacks a launch may hold.  The wave camera walk (its word stack lies past the lane stacks)
+    is refused and never chosen; the dry-run work map (8 counters per lane past the stacks) returns
+    RT_ERR_UNSUPPORTED, so a balancing attempt falls back to the measured cycle costs; frames --
+    primary+shadow and path-traced -- still equal the oracle's on the same tree."""
+    prims, mats, bvh = chain_scene(rt, 60)
+    g = rt.Scene(prims, mats, bvh=bvh)
+    assert g.info["depth"] >= 57
+    for walk in (rt.WALK_WAVE, rt.WALK_AUTO):
+        with pytest.raises(rt.RTError) as e:
+            g.set_camera_walk(walk)
+        assert e.value.code == rt.RT_ERR_UNSUPPORTED
+    o = oracle_scene(rt, oracle, prims, mats, bvh=bvh)
+    W, H = 160, 96
+    for depth in (1, 3):
+        r = rt.Renderer(g, W, H)
+        acc = np.zeros((W * H, 4), np.float32)
+        for fr in range(24):   # past the renderer's timed choices (the lane walk throughout)
+            got = r.tick_host(spp=1, depth=depth, frame=fr)
+            want, st = o.tick(W, H, acc, spp=1, depth=depth, frame=fr)
+            assert np.array_equal(got, want), (depth, fr)
+        gacc = np.ascontiguousarray(r.accumulator(), np.float32).reshape(-1, 4)
+        assert np.array_equal(gacc.view(np.uint32), acc.view(np.uint32))
+        if depth == 1:
+            assert r.choices()["walk"] == 0
+        with pytest.raises(rt.RTError) as e:
+            r.tile_work(spp=1, depth=depth, frame=0)
+        assert e.value.code == rt.RT_ERR_UNSUPPORTED
+        r.close()
+    g.close()
 
 
 def test_invalid_scenes_rejected(rt, torch):

@@ -40,6 +40,8 @@ def test_standin_library_exports_the_rccl_subset():
     (8, "pipelined", "teapotF", 1920, 1080),           # the driver's default N = 8 run (weak config 2 deal)
     (8, "balanced", "mig16", 1920, 1080),              # config 4 at N = 8: balanced + pipelined, two switches
     (8, "ptbal", "cfg5", 480, 270),                    # config 5's scene at N = 8: path-traced balanced deal
+    (8, "pt", "cfg5", 1920, 1080),                     # config 5 as the bench splits it: 1080p, 16 spp, depth 10
+    (2, "balanced", "chain60", 160, 96),               # a 61-level tree: no work map, cycle costs
 ])
 def test_multi_frame_world_n_on_one_gpu(world, mode, recipe, W, H):
     assert os.path.exists(STANDIN), "tests/cpp/libinproc_rccl.so must be built beforehand (__graft_entry__.build())"
@@ -78,7 +80,9 @@ def test_balanced_deal_is_reproducible(world, mode, recipe, W, H):
 def test_collective_failure_reaches_every_rank(site):
     """A local failure inside a per-frame collective (the cost exchange's block upload, the
     accumulator move's pack; RT_MULTI_FAULT injects it on one rank) makes rt_render_frame_multi
-    return an error on EVERY rank from the same call -- no rank is left waiting in the group."""
+    return an error on EVERY rank from the same call -- no rank is left waiting in the group -- and
+    the failed attempt is not retried: every later frame renders, and rank 0's frames equal Tick's
+    with the failed frame left out (the injected fault stays armed throughout)."""
     assert os.path.exists(STANDIN)
     env = dict(os.environ, RT_RCCL_LIB=STANDIN)
     p = subprocess.run([sys.executable, "-u", DRIVER, "3", "fault:" + site, "teapotF", "200", "120"], env=env,

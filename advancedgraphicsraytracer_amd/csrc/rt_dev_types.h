@@ -43,6 +43,7 @@ struct SceneView {
     uint32_t stack_entries;             // LDS stack entries per lane
     int wave_primary;                   // camera rays take the wave-coherent walk
     int walk_check;                     // RT_WALK_CHECK_*: what the walk counts / verifies
+    float walk_margin;                  // the wave walk enters a box whose entry is below t * (1 + walk_margin)
     const float4 *__restrict__ quads;   // two-level node records (8 float4 each, build_quads) or null
     uint32_t quad_root;                 // the root's record word
     int quad_lanes;                     // the lane kernel walks the two-level records

@@ -434,6 +434,47 @@ inline f3 tvec_host(float4 r0, float4 r1, float4 r2, f3 a) {
     return tvec(M, a);
 }
 
+// The wave camera walk's sticky boxes (rt_kernels.inc, wave_closest_hit_fast): a node with a
+// primitive below it whose computed t can lie well before its leaf box's entry -- a sliver
+// triangle (its smallest corner angle under 2^RT_WALK_STICKY rad, default 2^-10: the common
+// denominator of t, u, v is then mostly rounding, Primitive.h:255-273), a sphere (t = -b - sqrt(d)
+// near a tangent, Primitive.h:150-177) or a quad -- gets b.w = 1, and the walk culls it only on a
+// slab miss.  Computed in double on the float vertices; the lane traversals never read b.w.
+void mark_sticky(const Bvh &b, const rt_scene_desc *d, std::vector<float4> &nodes) {
+    double lim = std::ldexp(1.0, -10);
+    if (const char *e = std::getenv("RT_WALK_STICKY")) lim = std::atoi(e) >= 0 ? 0.0 : std::ldexp(1.0, std::atoi(e));
+    bool spheres = true;   // RT_WALK_STICKY_SPHERES=0: A/B only
+    if (const char *e = std::getenv("RT_WALK_STICKY_SPHERES")) spheres = std::atoi(e) != 0;
+    auto prim_sticky = [&](const rt_prim &p) {
+        if (p.type == RT_SPHERE || p.type == RT_QUAD) return spheres;
+        if (p.type != RT_TRIANGLE) return false;   // planes: an unbounded box, entered from inside
+        double v[3][3], e[3][3], len[3];
+        for (int k = 0; k < 3; ++k)
+            for (int a = 0; a < 3; ++a) v[k][a] = p.v[3 * k + a];
+        for (int k = 0; k < 3; ++k) {
+            for (int a = 0; a < 3; ++a) e[k][a] = v[(k + 1) % 3][a] - v[k][a];
+            len[k] = std::sqrt(e[k][0] * e[k][0] + e[k][1] * e[k][1] + e[k][2] * e[k][2]);
+        }
+        const double cx = e[0][1] * e[2][2] - e[0][2] * e[2][1], cy = e[0][2] * e[2][0] - e[0][0] * e[2][2],
+                     cz = e[0][0] * e[2][1] - e[0][1] * e[2][0];
+        const double area2 = std::sqrt(cx * cx + cy * cy + cz * cz);
+        std::sort(len, len + 3);
+        return !(area2 >= lim * len[1] * len[2]);   // sine of the smallest angle = 2 area / (two longest edges)
+    };
+    const uint32_t used = b.nodes_used;
+    std::vector<uint32_t> parent(used, ~0u);
+    for (uint32_t i = 0; i < used; ++i)
+        if (i != 1 && b.nodes[i].count == 0)
+            for (uint32_t c = b.nodes[i].leftFirst; c < b.nodes[i].leftFirst + 2; ++c) parent[c] = i;
+    for (uint32_t i = 0; i < used; ++i) {
+        const Node &nd = b.nodes[i];
+        if (i == 1 || nd.count == 0 || nodes[2 * i + 1].w != 0.0f) continue;
+        bool st = false;
+        for (uint32_t k = nd.leftFirst; k < nd.leftFirst + nd.count && !st; ++k) st = prim_sticky(d->prims[b.indices[k]]);
+        for (uint32_t j = i; st && j != ~0u && nodes[2 * j + 1].w == 0.0f; j = parent[j]) nodes[2 * j + 1].w = 1.0f;
+    }
+}
+
 int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (!d || !out || !d->prims || d->num_prims == 0 || !d->materials || d->num_materials == 0)
         return fail(RT_ERR_INVALID, "rt_scene_create: empty or null description");
@@ -521,7 +562,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (s->bvh.depth > 64) { delete s; return fail(RT_ERR_UNSUPPORTED, "BVH deeper than 64 (the reference's stack[64])"); }
     s->stack_depth = pick_stack(s->bvh.depth);
     // trees deeper than 60: the lane stacks (depth x 1 KB) leave no room for the walk's words
-    s->walk_fits = (size_t)s->stack_depth * (256u + 4u) * sizeof(uint32_t) <= kLdsLaunchMax;
+    s->walk_fits = (size_t)s->stack_depth * (256u + 4u * 2u) * sizeof(uint32_t) <= kLdsLaunchMax;
 
     // ---- device node array: packed (leftFirst << 8 | count) word in b.z
     std::vector<float4> nodes(2 * (size_t)s->bvh.nodes_used);
@@ -531,6 +572,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         nodes[2 * i] = make_float4(nd.mn[0], nd.mn[1], nd.mn[2], nd.mx[0]);
         nodes[2 * i + 1] = make_float4(nd.mx[1], nd.mx[2], ubits(word), 0.0f);
     }
+    mark_sticky(s->bvh, d, nodes);
     std::vector<float4> quads;
     uint32_t quad_root = 0;
     {
@@ -770,6 +812,9 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
                 if (!(ch.mn[a] >= nd.mn[a]) || !(ch.mx[a] <= nd.mx[a])) s->nested = false;
         }
     }
+    // the wave walk's cull margin: RT_WALK_MARGIN = its base-2 exponent
+    v.walk_margin = 0x1p-18f;
+    if (const char *e = std::getenv("RT_WALK_MARGIN")) v.walk_margin = std::ldexp(1.0f, std::max(-40, std::min(-1, std::atoi(e))));
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
     v.wave_primary = 0;
     const bool wave_ok = !s->has_cubes && s->nested && s->walk_fits;
@@ -788,9 +833,9 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 
 size_t stack_bytes(const rt_scene *s) { return (size_t)s->stack_depth * 256u * sizeof(uint32_t); }
 // launches whose camera rays may take the wave walk (SceneView::wave_primary) also hold each wave's
-// uniform stack of node words past the lane stacks (walk_words in rt_kernels.inc): 4 waves x depth
+// uniform stack of (node word, sticky) pairs past the lane stacks (walk_words in rt_kernels.inc): 4 waves x depth
 size_t walk_bytes(const rt_scene *s, const SceneView &v) {
-    return v.wave_primary ? (size_t)s->stack_depth * 4u * sizeof(uint32_t) : 0u;
+    return v.wave_primary ? (size_t)s->stack_depth * 4u * 2u * sizeof(uint32_t) : 0u;
 }
 // the compiled MAXD class a Trace depth runs in
 int max_depth_class(uint32_t depth) { return depth <= 1 ? 1 : depth <= 4 ? 4 : depth <= 10 ? 10 : 32; }

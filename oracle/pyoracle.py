@@ -80,6 +80,7 @@ def lib():
         L.or_camera_rays.argtypes = [C.POINTER(Camera), C.c_int, C.c_int, C.c_int, ip, C.c_int, fp]
         L.or_pixel_work.argtypes = [vp, C.POINTER(Camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.c_int,
                                     C.POINTER(C.c_uint32)]
+        L.or_walk_need.argtypes = [vp, C.POINTER(Camera), C.c_int, C.c_int, C.c_int, ip, C.c_int, C.c_int, fp, ip]
         L.or_intersect.argtypes = [vp, fp, C.c_int, fp, ip, fp, fp, C.c_int]
         L.or_intersect_packets.argtypes = [vp, fp, C.c_int, fp, ip, fp, fp]
         L.or_occluded.argtypes = [vp, fp, C.c_int, C.POINTER(C.c_uint8)]
@@ -195,6 +196,19 @@ class Scene:
                              _p(out, C.c_uint32))
         return out
 
+    def walk_need(self, W, H, pixels=None, frame=0, cam=None, all_hits=False, with_obj=False):
+        """Per camera ray (sample 0 of `frame`): the cull margin the wave camera walk needs to return
+        IntersectBVH's answer R -- (entry of R's leaf box - t_R) / t_R, 0 if R lies at or past it
+        (or_walk_need); all_hits: the max of that over every primitive the ray hits; with_obj: also
+        R's primitive id per ray."""
+        pixels = np.arange(W * H, dtype=np.int32) if pixels is None else np.ascontiguousarray(pixels, np.int32)
+        out = np.zeros(len(pixels), np.float32)
+        obj = np.full(len(pixels), -1, np.int32)
+        c = self.camera(W, H) if cam is None else self.camera_from(W, H, cam)
+        self.L.or_walk_need(self.h, C.byref(c), W, H, frame, _p(pixels, C.c_int32), len(pixels), int(all_hits),
+                            _p(out, C.c_float), _p(obj, C.c_int32) if with_obj and not all_hits else None)
+        return (out, obj) if with_obj else out
+
     def trace_rays(self, rays, seeds, depth=10, flags=None):
         """Renderer::Trace / WhittedTrace (set_integrator) on (n, 7) rays with per-ray RNG states;
         returns (radiance [n, 3], seeds after the call, stats)."""
@@ -207,12 +221,24 @@ class Scene:
                              _p(seeds, C.c_uint32), _p(rgb, C.c_float), C.byref(st))
         return rgb, seeds, st.as_dict()
 
-    def tick(self, W, H, acc, spp=1, depth=10, frame=0, y0=0, y1=None, threads=0):
-        """One Renderer::Tick over rows [y0, y1): updates acc (H*W*4 f32) in place, returns RGB8."""
+    @classmethod
+    def camera_from(cls, W, H, cam):
+        """The default camera of a W x H frame with the position / screen corners / lens radius of
+        `cam` (an object with pos, top_left, top_right, bottom_left, lens_radius: the library's
+        rt.Camera) -- a moved camera as Camera::AdjustCamera leaves it (camera.h:54-86)."""
+        c = cls.camera(W, H)
+        for a, b in (("pos", "pos"), ("tl", "top_left"), ("tr", "top_right"), ("bl", "bottom_left")):
+            getattr(c, a)[:] = list(getattr(cam, b))
+        c.lens_radius = cam.lens_radius
+        return c
+
+    def tick(self, W, H, acc, spp=1, depth=10, frame=0, y0=0, y1=None, threads=0, cam=None):
+        """One Renderer::Tick over rows [y0, y1): updates acc (H*W*4 f32) in place, returns RGB8.
+        cam: a moved camera (camera_from), else the default one."""
         y1 = H if y1 is None else y1
         out = np.zeros(W * H, np.uint32)
         st = Stats()
-        cam = self.camera(W, H)
+        cam = self.camera(W, H) if cam is None else self.camera_from(W, H, cam)
         self.L.or_tick(self.h, C.byref(cam), W, H, spp, depth, frame, y0, y1, _p(acc, C.c_float),
                        _p(out, C.c_uint32), C.byref(st), threads)
         return out, st.as_dict()

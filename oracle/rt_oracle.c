@@ -1382,6 +1382,67 @@ void or_pixel_work(const or_scene *s, const or_camera *c, int W, int H, int spp,
     }
 }
 
+/* The wave camera walk's exactness precondition (the library's wave_closest_hit_fast,
+ * rt_kernels.inc).  The walk returns IntersectBVH's answer R for a camera ray, or flags the lane and
+ * re-traces it in the reference order, unless R's computed t_R lies at least the walk's cull margin
+ * before the computed slab entry of R's own leaf box L_R: e_L >= t_R * (1 + margin).  Per camera ray
+ * (sample 0 of `frame`) this returns need = (e_L - t_R) / t_R for R = the reference's answer (0 for a
+ * miss or a hit at or past its leaf's entry).  all != 0: the max of the same quantity over EVERY
+ * primitive the ray hits (Primitive::Intersect accepting it from a fresh ray), found by a traversal
+ * that culls boxes only on a slab miss -- a bound for any visiting order.  A frame whose rays all have
+ * need < margin is rendered by the walk exactly as by the reference order.  obj (optional, all == 0):
+ * R's primitive id per ray (-1 for a miss). */
+void or_walk_need(const or_scene *s, const or_camera *c, int W, int H, int frame, const int32_t *pixels, int n,
+                  int all, float *need, int32_t *obj) {
+    #pragma omp parallel for schedule(dynamic, 64)
+    for (int i = 0; i < n; i++) {
+        uint32_t seed = pixel_seed(W, H, pixels[i], 0, 1, frame);
+        const ray_t r = primary_ray(c, pixels[i] % W, pixels[i] / W, &seed);
+        int target = -1;
+        float t_target = 0.0f;
+        if (!all) {
+            ray_t q = r;
+            intersect_bvh(s, &q, NULL);
+            target = q.obj;
+            t_target = q.t;
+            if (obj) obj[i] = target;
+            if (target < 0) { need[i] = 0.0f; continue; }
+        }
+        const node *stack[64];
+        uint32_t sp = 0;
+        const node *nd = &s->nodes[0];
+        double worst = 0.0;
+        for (;;) {
+            if (nd->count > 0) {
+                const float e = slab_entry(&r, nd);
+                for (uint32_t k = 0; k < nd->count; k++) {
+                    int oi = (int)s->idx[nd->leftFirst + k];
+                    if (!all && oi != target) continue;
+                    float tp = t_target;
+                    if (all) {
+                        ray_t q = r;
+                        prim_intersect(&s->p[oi], &q, oi);
+                        if (q.obj != oi) continue;
+                        tp = q.t;
+                    }
+                    if (e > tp) {
+                        double d = ((double)e - (double)tp) / (double)tp;
+                        if (d > worst) worst = d;
+                    }
+                }
+            } else {
+                const node *c1 = &s->nodes[nd->leftFirst], *c2 = &s->nodes[nd->leftFirst + 1];
+                int h1 = hits_aabb(&r, c1), h2 = hits_aabb(&r, c2);   /* r.t = 1e34: a miss only */
+                if (h1 && h2) { nd = c1; stack[sp++] = c2; continue; }
+                if (h1 || h2) { nd = h1 ? c1 : c2; continue; }
+            }
+            if (sp == 0) break;
+            nd = stack[--sp];
+        }
+        need[i] = (float)worst;
+    }
+}
+
 void or_trace_pixels(const or_scene *s, const or_camera *c, int W, int H, int spp, int depth, int frame,
                      const int32_t *pixels, int n, float *rgb, or_stats *st) {
     #pragma omp parallel

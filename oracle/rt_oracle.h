@@ -117,6 +117,9 @@ void or_trace_pixels(const or_scene *s, const or_camera *c, int W, int H, int sp
  * rays counted in the library's farther-box-first order), closest-hit pops of interior / leaf
  * entries whose pushed entry distance is >= the ray's t at the pop, 0, 0 -- summed over the
  * pixel's samples */
+/* the wave camera walk's exactness precondition per camera ray (see rt_oracle.c) */
+void or_walk_need(const or_scene *s, const or_camera *c, int W, int H, int frame, const int32_t *pixels, int n,
+                  int all, float *need, int32_t *obj);
 void or_pixel_work(const or_scene *s, const or_camera *c, int W, int H, int spp, int depth, int frame,
                    const int32_t *pixels, int n, uint32_t *work);
 /* One Renderer::Tick over rows [y0,y1): trace, running average into acc (float4 per

@@ -33,7 +33,7 @@ MODE: sync | pipelined -- the interleaved deal;
                   error from the same call and none may be left waiting in the collective; the
                   frames after it render (the failed attempt is not retried) and equal
                   Tick's frames with the failed one left out.
-RECIPE: a bench recipe, or chain60 (tests/scenes_util.chain_scene: a 61-level prebuilt tree whose
+RECIPE: a bench recipe, or chain64 (tests/scenes_util.chain_scene: a 64-level prebuilt tree whose
         dry-run work map is unsupported, so balancing falls back to measured cycle costs).
 The balanced modes print the communicator's deal_info and deal hash (equal on every rank) and
 require the balanced deal at the end."""
@@ -54,9 +54,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
 def make_scene(recipe):
-    if recipe == "chain60":
+    if recipe == "chain64":
         from scenes_util import chain_scene
-        prims, mats, bvh = chain_scene(rt, 60)
+        prims, mats, bvh = chain_scene(rt, 64)
         return rt.Scene(prims, mats, bvh=bvh)
     return rt.Scene.recipe(recipe)
 

@@ -130,10 +130,10 @@ def kat_rays():
     return np.concatenate([rays, cloud], 0)
 
 
-def chain_scene(rt, n_tris=60):
+def chain_scene(rt, n_tris=64):
     """A caterpillar tree one primitive per level: the light (prim 0) and n_tris small
     diffuse triangles in front of the default camera, with a prebuilt BVH whose every interior node
-    has a leaf child and an interior child -- depth n_tris + 1 (61 by default), so the LDS stacks
+    has a leaf child and an interior child -- depth n_tris (64, the most a scene may have), so the LDS stacks
     fill 64 KB (64 entries x 256 lanes x 4 B) and leave no room for the wave walk's words or the work
     map's counters.  Boxes are the unions of their primitives' boxes (nested).  Returns prims,
     materials, (nodes [n, 32] uint8, indices)."""
@@ -171,3 +171,66 @@ def chain_scene(rt, n_tris=60):
         else:
             put(3 + 2 * j, *union(j + 1), 4 + 2 * j, 0)
     return prims, mats, (nodes.view(np.uint8).reshape(len(nodes), 32), np.arange(P, dtype=np.uint32))
+
+
+def _cam(rt, W, H, pos, fwd, right, up):
+    """A pinhole camera looking along fwd from pos, the screen one unit ahead spanning
+    [-aspect, aspect] x [-1, 1] along right / up (the default camera's shape, camera.h:28-41)."""
+    c = rt.Camera.default(W, H)
+    pos, fwd, right, up = (np.asarray(v, np.float64) for v in (pos, fwd, right, up))
+    a = W / H
+    ctr = pos + fwd
+    for name, p in (("pos", pos), ("top_left", ctr - a * right + up), ("top_right", ctr + a * right + up),
+                    ("bottom_left", ctr - a * right - up)):
+        getattr(c, name)[:] = [float(np.float32(x)) for x in p]
+    return c
+
+
+def grazing_cameras(rt, W, H):
+    """Cameras aimed at the wave walk's open case: camera rays that graze a
+    triangle's plane, where the computed triangle t carries the most rounding error relative to its
+    leaf box's entry.  TEAPOT-F: the eye at the floor's height (y = -1.225) looking along the floor,
+    and just above it looking slightly down (every floor hit grazing); mig29 x16: the eye in the plane
+    of the largest triangle of the first aircraft (a wing), looking at that triangle, with the
+    image's middle row in the plane."""
+    out = {}
+    y = -1.225
+    out["teapotF_floor_level"] = ("teapotF", _cam(rt, W, H, (0.0, y, -1.0), (0, 0, 1), (1, 0, 0), (0, 1, 0)))
+    f = np.array([0.0, -0.02, 1.0])
+    f /= np.linalg.norm(f)
+    up = np.cross(f, (1.0, 0.0, 0.0))
+    out["teapotF_floor_skim"] = ("teapotF", _cam(rt, W, H, (0.3, y + 0.02, -1.0), f, (1, 0, 0), -up))
+    prims, _ = rt.recipe_describe("mig16")
+    n1 = 1 + (len(prims) - 1) // 16           # the first aircraft's triangles
+    best, area = None, -1.0
+    for p in prims[1:n1]:
+        v = np.array(list(p.v)[:9], np.float64).reshape(3, 3)
+        ar = 0.5 * np.linalg.norm(np.cross(v[1] - v[0], v[2] - v[0]))
+        if ar > area:
+            best, area = v, ar
+    ctr = best.mean(axis=0)
+    n = np.cross(best[1] - best[0], best[2] - best[0])
+    n /= np.linalg.norm(n)
+    d = ctr - np.array([0.0, 0.0, -1.0])      # from the default eye, projected into the plane
+    d -= n * d.dot(n)
+    d /= np.linalg.norm(d)
+    right = np.cross(n, d)
+    out["mig16_wing_plane"] = ("mig16", _cam(rt, W, H, ctr - 1.5 * d, d, right, n))
+    return out
+
+
+def sticky_prims(rt, prims, log2_lim=-10):
+    """The primitives whose boxes the wave camera walk never culls by distance (rt_device.hip
+    mark_sticky): spheres, quads and sliver triangles (smallest corner angle's sine under
+    2^log2_lim, from the float vertices in double)."""
+    out = np.zeros(len(prims), bool)
+    lim = 2.0 ** log2_lim
+    for i, p in enumerate(prims):
+        if p.type in (rt.SPHERE, rt.QUAD):
+            out[i] = True
+        elif p.type == rt.TRIANGLE:
+            v = np.array(list(p.v)[:9], np.float64).reshape(3, 3)
+            e = [v[(k + 1) % 3] - v[k] for k in range(3)]
+            ln = sorted(float(np.linalg.norm(x)) for x in e)
+            out[i] = not (np.linalg.norm(np.cross(e[0], e[2])) >= lim * ln[1] * ln[2])
+    return out

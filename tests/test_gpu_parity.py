@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-from scenes_util import chain_scene, oracle_scene
+from scenes_util import chain_scene, grazing_cameras, oracle_scene
 
 pytestmark = pytest.mark.gpu
 
@@ -346,14 +346,14 @@ def test_wave_walk_needs_nested_boxes(rt, oracle, scenes, torch):
 
 
 def test_deep_prebuilt_tree_keeps_to_64kb_of_lds(rt, oracle, torch):
-    """a prebuilt tree 61 levels deep (tests/scenes_util.chain_scene) fills the 64 KB of
+    """a prebuilt tree 64 levels deep (tests/scenes_util.chain_scene) fills the 64 KB of
     lane stacks a launch may hold.  The wave camera walk (its word stack lies past the lane stacks)
     is refused and never chosen; the dry-run work map (8 counters per lane past the stacks) returns
     RT_ERR_UNSUPPORTED, so a balancing attempt falls back to the measured cycle costs; frames --
     primary+shadow and path-traced -- still equal the oracle's on the same tree."""
-    prims, mats, bvh = chain_scene(rt, 60)
+    prims, mats, bvh = chain_scene(rt, 64)
     g = rt.Scene(prims, mats, bvh=bvh)
-    assert g.info["depth"] >= 57
+    assert g.info["depth"] == 64
     for walk in (rt.WALK_WAVE, rt.WALK_AUTO):
         with pytest.raises(rt.RTError) as e:
             g.set_camera_walk(walk)
@@ -871,6 +871,38 @@ def test_wave_walk_config4_full_size_bit_exact(rt, scenes, W, H, frames):
     assert ws["walked"] == 2 * W * H
     assert ws["verify_mismatch"] == 0, ws
     r.close()
+
+
+@pytest.mark.parametrize("cam_name", ["teapotF_floor_level", "teapotF_floor_skim", "mig16_wing_plane"])
+def test_wave_walk_grazing_cameras_bit_exact(rt, oracle, cam_name):
+    """cameras aimed at the wave walk's open case (tests/scenes_util.grazing_cameras --
+    the eye at the floor's height looking along it, just above it looking down, and in the plane of
+    a mig29 wing), 1080p, the walk forced and RT_WALK_CHECK_VERIFY on: every walked lane is re-traced
+    in the reference order and compared (no lane may differ), and every frame's RGB8 and accumulator
+    bits equal the oracle's.  The wing-plane camera's frame 0 holds a ray whose reference answer is
+    a sliver triangle 2^-8 before its leaf box's entry (tests/test_walk_certificate.py): its boxes
+    are sticky, so the walk cannot hide it."""
+    W, H, frames = 1920, 1080, 3
+    rec, cam = grazing_cameras(rt, W, H)[cam_name]
+    g = rt.Scene.recipe(rec)
+    g.set_camera_walk(rt.WALK_WAVE)
+    o = oracle.Scene(rec, rt.DATA_DIR)
+    r = rt.Renderer(g, W, H)
+    r.camera = cam
+    r.set_walk_check(rt.WALK_CHECK_VERIFY)
+    acc = np.zeros((W * H, 4), np.float32)
+    for f in range(frames):
+        got = r.tick_host(spp=1, depth=1, frame=f)
+        want, _ = o.tick(W, H, acc, spp=1, depth=1, frame=f, cam=cam)
+        assert np.array_equal(got, want), f"frame {f}: {(got != want).sum()} RGB8 mismatches"
+    assert_acc_bits(r.accumulator(), acc)
+    ws = r.walk_stats()
+    print(f"{cam_name}: {ws}")
+    # a wave with a non-finite 1/D (a ray exactly parallel to an axis) takes the lane walk
+    assert 0.999 * frames * W * H <= ws["walked"] <= frames * W * H
+    assert ws["verify_mismatch"] == 0, ws
+    r.close()
+    g.close()
 
 
 def test_wave_walk_config4_balanced_eighth_shard_bit_exact(rt, scenes):

@@ -41,7 +41,7 @@ def test_standin_library_exports_the_rccl_subset():
     (8, "balanced", "mig16", 1920, 1080),              # config 4 at N = 8: balanced + pipelined, two switches
     (8, "ptbal", "cfg5", 480, 270),                    # config 5's scene at N = 8: path-traced balanced deal
     (8, "pt", "cfg5", 1920, 1080),                     # config 5 as the bench splits it: 1080p, 16 spp, depth 10
-    (2, "balanced", "chain60", 160, 96),               # a 61-level tree: no work map, cycle costs
+    (2, "balanced", "chain64", 160, 96),               # a 64-level tree: no work map, cycle costs
 ])
 def test_multi_frame_world_n_on_one_gpu(world, mode, recipe, W, H):
     assert os.path.exists(STANDIN), "tests/cpp/libinproc_rccl.so must be built beforehand (__graft_entry__.build())"

@@ -1,9 +1,8 @@
 set -o pipefail
-mkdir -p gpurun_out/r6a
+mkdir -p gpurun_out/r6d
 run() { echo "== $1"; shift; timeout -k 10 "$@"; }
 export PYTHONUNBUFFERED=1
-run bench_default 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r6a/bench_default.json 2> gpurun_out/r6a/bench_default.err && \
-run gloo2 300 env RT_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 5 --extra-configs "" > gpurun_out/r6a/bench_gloo2.json 2> gpurun_out/r6a/bench_gloo2.err && \
-run tests 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "deep_prebuilt or nested" tests/test_multi_inproc.py -k "chain60 or fault or pt-cfg5 or deep_prebuilt or nested" > gpurun_out/r6a/tests.log 2>&1 && \
-run bench_hwq8 300 python -u bench.py --steps 20 --warmup 5 --hw-queues 8 --no-cpu-baseline > gpurun_out/r6a/bench_hwq8.json 2> gpurun_out/r6a/bench_hwq8.err && \
-run bench_default2 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/r6a/bench_default2.json 2> gpurun_out/r6a/bench_default2.err
+V="--var RT_WAVE_PRIMARY=1,RT_WALK_STICKY=0 --var RT_WAVE_PRIMARY=1,RT_WALK_STICKY=-10 --var RT_WAVE_PRIMARY=1,RT_WALK_STICKY=-14 --var RT_WAVE_PRIMARY=1,RT_WALK_STICKY=-14,RT_WALK_STICKY_SPHERES=0 --var RT_WAVE_PRIMARY=1,RT_WALK_STICKY=0,RT_WALK_STICKY_SPHERES=1 --var RT_WAVE_PRIMARY=0"
+run ab1 300 env RT_PS_PIPELINE=0 python -u tools/knob_ab.py --scene mig16 --spp 1 --depth 1 --rounds 15 --frames 20 --check $V > gpurun_out/r6d/ab_serial.log 2>&1 && \
+run ab2 300 python -u tools/knob_ab.py --scene mig16 --spp 1 --depth 1 --rounds 15 --frames 20 --check $V > gpurun_out/r6d/ab_pipe.log 2>&1 && \
+run verify 300 python -u tools/walk_verify.py --frames 2 --var RT_WALK_STICKY=-14 --var RT_WALK_STICKY=-14,RT_WALK_STICKY_SPHERES=0 > gpurun_out/r6d/walk_verify.jsonl 2> gpurun_out/r6d/walk_verify.err

@@ -67,7 +67,8 @@ struct rt_scene {
                                 // plain build, 8 = the single-sample one wherever it applies (RT_FRAME_WAVES)
     uint32_t num_cus = 256;     // CUs of the device (resident grids, frames-in-flight rules)
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
-    bool quads = false;         // two-level node records built (RT_PT_QUADS=1, build_quads); the lane kernel walks them
+    bool quads = false;         // two-level node records built (build_quads): the wave camera walk takes them
+    bool quad_lanes = false;    // ... and the lane kernel too (RT_PT_QUADS=1)
     void *d_quads = nullptr;
     bool walk_fits = true;      // the lane stacks + the wave walk's word stack fit one launch's LDS (kLdsLaunchMax)
     bool nested = true;         // every child box lies inside its parent's (as floats): the wave walk's
@@ -302,7 +303,7 @@ constexpr int kTuneRestarts = 4;
 // marker ((kQuadOdd | record << 1 | half) << 8).  false (no records) when a box is NaN, a parent is
 // not the exact union of its children (a caller's prebuilt tree), or the tree is too large.
 constexpr uint32_t kQuadOdd = 1u << 23;
-bool build_quads(const Bvh &b, std::vector<float4> &rec, uint32_t &root_word) {
+bool build_quads(const Bvh &b, const std::vector<uint8_t> &sticky, std::vector<float4> &rec, uint32_t &root_word) {
     const Node *N = b.nodes.data();
     if (b.nodes_used < 3 || N[0].count > 0) return false;
     std::vector<int32_t> id(b.nodes_used, -1);
@@ -332,6 +333,8 @@ bool build_quads(const Bvh &b, std::vector<float4> &rec, uint32_t &root_word) {
         q[0] = make_float4(nd.mn[0], nd.mn[1], nd.mn[2], nd.mx[0]);
         q[1] = make_float4(nd.mx[1], nd.mx[2], ubits(w), 0.0f);
     };
+    // the .w word of each entry: bit 0 (first slot of a half) the child is a leaf and this its entry,
+    // bit 1 this entry's node is sticky (mark_sticky), bit 2 (first slot) the child itself is sticky
     rec.assign(8 * order.size(), make_float4(0, 0, 0, 0));
     for (size_t r = 0; r < order.size(); ++r) {
         const Node &x = N[order[r]];
@@ -339,9 +342,10 @@ bool build_quads(const Bvh &b, std::vector<float4> &rec, uint32_t &root_word) {
             const uint32_t c = x.leftFirst + h;
             float4 *q = &rec[8 * r + 4 * h];
             const Node &cn = N[c];
+            const uint32_t sc = sticky[c] ? 6u : 0u;
             if (cn.count > 0) {
                 entry(c, q);
-                q[1].w = ubits(1u);
+                q[1].w = ubits(1u | sc);
                 continue;
             }
             const Node &g1 = N[cn.leftFirst], &g2 = N[cn.leftFirst + 1];
@@ -349,6 +353,8 @@ bool build_quads(const Bvh &b, std::vector<float4> &rec, uint32_t &root_word) {
                 if (!pick(g1.mn[a], g2.mn[a], true, cn.mn[a]) || !pick(g1.mx[a], g2.mx[a], false, cn.mx[a])) return false;
             entry(cn.leftFirst, q);
             entry(cn.leftFirst + 1, q + 2);
+            q[1].w = ubits((sticky[cn.leftFirst] ? 2u : 0u) | (sc & 4u));
+            q[3].w = ubits(sticky[cn.leftFirst + 1] ? 2u : 0u);
         }
     }
     root_word = (uint32_t)id[0] << 8;
@@ -440,7 +446,7 @@ inline f3 tvec_host(float4 r0, float4 r1, float4 r2, f3 a) {
 // denominator of t, u, v is then mostly rounding, Primitive.h:255-273), a sphere (t = -b - sqrt(d)
 // near a tangent, Primitive.h:150-177) or a quad -- gets b.w = 1, and the walk culls it only on a
 // slab miss.  Computed in double on the float vertices; the lane traversals never read b.w.
-void mark_sticky(const Bvh &b, const rt_scene_desc *d, std::vector<float4> &nodes) {
+void mark_sticky(const Bvh &b, const rt_scene_desc *d, std::vector<float4> &nodes, std::vector<uint8_t> &sticky) {
     double lim = std::ldexp(1.0, -10);
     if (const char *e = std::getenv("RT_WALK_STICKY")) lim = std::atoi(e) >= 0 ? 0.0 : std::ldexp(1.0, std::atoi(e));
     bool spheres = true;   // RT_WALK_STICKY_SPHERES=0: A/B only
@@ -473,6 +479,8 @@ void mark_sticky(const Bvh &b, const rt_scene_desc *d, std::vector<float4> &node
         for (uint32_t k = nd.leftFirst; k < nd.leftFirst + nd.count && !st; ++k) st = prim_sticky(d->prims[b.indices[k]]);
         for (uint32_t j = i; st && j != ~0u && nodes[2 * j + 1].w == 0.0f; j = parent[j]) nodes[2 * j + 1].w = 1.0f;
     }
+    sticky.assign(used, 0);
+    for (uint32_t i = 0; i < used; ++i) sticky[i] = nodes[2 * i + 1].w != 0.0f;
 }
 
 int scene_create(const rt_scene_desc *d, rt_scene **out) {
@@ -572,13 +580,17 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         nodes[2 * i] = make_float4(nd.mn[0], nd.mn[1], nd.mn[2], nd.mx[0]);
         nodes[2 * i + 1] = make_float4(nd.mx[1], nd.mx[2], ubits(word), 0.0f);
     }
-    mark_sticky(s->bvh, d, nodes);
+    std::vector<uint8_t> sticky;
+    mark_sticky(s->bvh, d, nodes, sticky);
     std::vector<float4> quads;
     uint32_t quad_root = 0;
     {
-        bool want = RT_PT_QUADS_DEFAULT != 0;
-        if (const char *e = std::getenv("RT_PT_QUADS")) want = std::atoi(e) != 0;
-        s->quads = want && build_quads(s->bvh, quads, quad_root);
+        bool lanes = RT_PT_QUADS_DEFAULT != 0, walk = true;   // RT_WALK_QUADS=0: the binary wave walk
+        if (const char *e = std::getenv("RT_PT_QUADS")) lanes = std::atoi(e) != 0;
+        if (const char *e = std::getenv("RT_WALK_QUADS")) walk = std::atoi(e) != 0;
+        s->quads = (lanes || walk) && build_quads(s->bvh, sticky, quads, quad_root);
+        s->quad_lanes = s->quads && lanes;
+        s->view.quad_walk = s->quads && walk ? 1 : 0;
     }
     // ---- leaf-order primitive records and per-id shading records; cubes and quads keep
     // their matrices and data in a side table (8 float4 each)
@@ -956,7 +968,7 @@ int launch_pt_frame(rt_renderer *r, const FrameArgs &F, SceneView view, bool tex
                         (s->walk == RT_WALK_WAVE || (s->walk == RT_WALK_AUTO && r->tune == kTuneDone && r->wave));
     view.walk_stats = r->d_counters;
     view.walk_check = r->walk_check;
-    view.quad_lanes = s->quads ? 1 : 0;
+    view.quad_lanes = s->quad_lanes ? 1 : 0;
     const uint64_t npix = (uint64_t)F.ntiles_local * 64u;
     // pipelined: per-sample results of the whole frame in a frame-level buffer (two by frame
     // parity, up to 2 GB each); the serial path keeps them per batch with a running sum

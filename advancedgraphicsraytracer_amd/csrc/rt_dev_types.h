@@ -47,7 +47,6 @@ struct SceneView {
     const float4 *__restrict__ quads;   // two-level node records (8 float4 each, build_quads) or null
     uint32_t quad_root;                 // the root's record word
     int quad_lanes;                     // the lane kernel walks the two-level records
-    int quad_walk;                      // the wave camera walk takes the two-level records
     unsigned long long *walk_stats;     // the renderer's counter slots (kCounterSlots x 8 u64), set per
                                         // launch: the wave walk adds [2] boxes entered within its
                                         // cull margin, [3] lanes re-traced in the reference order,

@@ -67,8 +67,8 @@ struct rt_scene {
                                 // plain build, 8 = the single-sample one wherever it applies (RT_FRAME_WAVES)
     uint32_t num_cus = 256;     // CUs of the device (resident grids, frames-in-flight rules)
     bool has_cubes = false;     // cube acceptance depends on the visiting order: no wave walk
-    bool quads = false;         // two-level node records built (build_quads): the wave camera walk takes them
-    bool quad_lanes = false;    // ... and the lane kernel too (RT_PT_QUADS=1)
+    bool quads = false;         // two-level node records built (RT_PT_QUADS=1, build_quads)
+    bool quad_lanes = false;    // ... and the lane kernel walks them
     void *d_quads = nullptr;
     bool walk_fits = true;      // the lane stacks + the wave walk's word stack fit one launch's LDS (kLdsLaunchMax)
     bool nested = true;         // every child box lies inside its parent's (as floats): the wave walk's
@@ -585,12 +585,10 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     std::vector<float4> quads;
     uint32_t quad_root = 0;
     {
-        bool lanes = RT_PT_QUADS_DEFAULT != 0, walk = true;   // RT_WALK_QUADS=0: the binary wave walk
+        bool lanes = RT_PT_QUADS_DEFAULT != 0;
         if (const char *e = std::getenv("RT_PT_QUADS")) lanes = std::atoi(e) != 0;
-        if (const char *e = std::getenv("RT_WALK_QUADS")) walk = std::atoi(e) != 0;
-        s->quads = (lanes || walk) && build_quads(s->bvh, sticky, quads, quad_root);
-        s->quad_lanes = s->quads && lanes;
-        s->view.quad_walk = s->quads && walk ? 1 : 0;
+        s->quads = lanes && build_quads(s->bvh, sticky, quads, quad_root);
+        s->quad_lanes = s->quads;
     }
     // ---- leaf-order primitive records and per-id shading records; cubes and quads keep
     // their matrices and data in a side table (8 float4 each)

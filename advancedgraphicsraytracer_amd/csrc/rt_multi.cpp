@@ -806,6 +806,11 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
             }
             if (!c->settled && c->pcalls == c->next_try) {
                 bool complete = false;
+                // the attempt's dry-run work map runs on the communicator's stream: behind the
+                // caller's frames in flight, not beside them (ADVICE r5 -- it would share the CUs
+                // with them and skew the renderer's timed groups)
+                HIP_TRY(hipEventRecord(c->ev_caller, st));
+                HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_caller, 0));
                 if ((rc = rebalance(c, r, cam, p, next, complete)) != RT_OK) {
                     // failed on every rank alike (the status words): the parameter set settles on
                     // the deal in use instead of retrying a failure every later frame

@@ -423,9 +423,9 @@ def extra_config(cfg_no, world, rank, device, dist, stream, summary, warm_s=1.5,
         res.update(path="rt_render_frame_multi (pipelined, %s)" % ("RT_MULTI_BALANCED" if ec["balanced"] else "interleaved deal"),
                    deal_rank0={"in_use": "balanced" if di["balanced"] else "interleaved", **di},
                    render_ms_per_frame_by_rank=[round(e[0].item(), 4) for e in every],
-                   # rank 0's gather is its receives on the communicator's stream behind its own render:
-                   # the exposed part is not separable from the render there, so it is not reported
-                   gather_ms_per_frame_by_rank=[None] + [round(e[1].item(), 4) for e in every[1:]])
+                   # per rank max(0, gather end - render end); rank 0 receives without waiting for its own
+                   # render, so its figure is how much later than its own tiles the peers' arrived
+                   gather_ms_per_frame_by_rank=[round(e[1].item(), 4) for e in every])
         sf.close()
     else:
         res.update(path="Renderer.Tick", in_flight=rx.overlap_depth()[0])

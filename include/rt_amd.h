@@ -302,8 +302,11 @@ int rt_render_frame_multi(rt_renderer *r, rt_comm *c, const rt_camera *cam, cons
                           uint32_t *rgb8_dev, uint32_t flags, void *stream);
 int rt_multi_flush(rt_renderer *r, rt_comm *c, uint32_t *rgb8_dev, void *stream);
 /* Sum over the RT_MULTI_TIMING frames since the last call (waits for them): render_ms =
- * this rank's shard render, gather_ms = from the render's end to the gather's completion
- * (exposed exchange latency; beside the next render in pipelined mode); resets the sums. */
+ * this rank's shard render, gather_ms = from the render's end to the gather's completion,
+ * max(0, ...) per frame (exposed exchange latency; beside the next render in pipelined mode).
+ * Pipelined rank 0 receives on the communicator's stream without waiting for its own render,
+ * so its figure is how much later than its own tiles the peers' tiles arrived (0 when they
+ * were there first); resets the sums. */
 int rt_comm_timing(rt_comm *c, double *render_ms, double *gather_ms, uint64_t *frames);
 /* The deal frames are rendered under now (every argument but c may be NULL): *balanced = 1 for a
  * cost-balanced deal, 0 for the interleaved one; *ntiles = this rank's tile count and tile_list

@@ -822,7 +822,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
                 if (!(ch.mn[a] >= nd.mn[a]) || !(ch.mx[a] <= nd.mx[a])) s->nested = false;
         }
     }
-    // the wave walk's cull margin (DESIGN 4b): RT_WALK_MARGIN = its base-2 exponent
+    // the wave walk's cull margin (DESIGN 2.3): RT_WALK_MARGIN = its base-2 exponent
     v.walk_margin = 0x1p-18f;
     if (const char *e = std::getenv("RT_WALK_MARGIN")) v.walk_margin = std::ldexp(1.0f, std::max(-40, std::min(-1, std::atoi(e))));
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)

@@ -193,7 +193,7 @@ CONFIGS = {
 # Algorithmic bytes per ray, SURVEY.md 8(d): B = 32*A + 40*P (+36 B pixel IO per camera
 # sample), A = BVH node reads (one 32-B node per child test), P = primitive tests (4-B index
 # + 36-B triangle).  A, P measured with the oracle on these workloads (per-pixel seeds, Trace
-# depth 1); DESIGN.md section 4.  Not a roofline: those bytes are L1/L2 hits.
+# depth 1); DESIGN.md section 5.  Not a roofline: those bytes are L1/L2 hits.
 BYTES_PER_RAY = {
     "teapotF": (32 * 14.235 + 40 * 1.635 + 36, 32 * 16.719 + 40 * 2.133),
     "mig16": (32 * 23.241 + 40 * 1.835 + 36, 32 * 79.366 + 40 * 8.545),
@@ -339,7 +339,7 @@ def extra_config(cfg_no, world, rank, device, dist, stream, summary, warm_s=1.5,
     primary + shadow) is north_star's strong-scaling case -- ONE frame split over the N ranks with the
     cost-balanced deal (RT_MULTI_BALANCED); config 3 (CFG3-sub, 4 spp, depth 4) is weak (each rank a
     1/N shard at spp 4N, interleaved deal); config 5 (CFG5-sub, 16 spp, depth 10) is strong (one
-    frame split, interleaved deal: the bounce levels' cost is not the camera rays', DESIGN 5).  All go
+    frame split, interleaved deal: the bounce levels' cost is not the camera rays', DESIGN 6.2).  All go
     through rt_render_frame_multi (pipelined) at N > 1 and through Tick at N = 1.
     Warm-up: blocks of frames until warm_s seconds have passed (and, for config 4 at N > 1, every
     rank renders under the balanced deal; the renderer's timed choices re-run on the new deal's
@@ -494,7 +494,7 @@ def main():
             # hold its region's part of the scene); weak scaling keeps the interleaved deal, whose
             # 1/N shards at spp N are statistically identical, and so do path-traced frames: the
             # level-0 cost deal measured slower than interleaving on config 5 (1/8 shard 1.56 vs
-            # 1.31 ms, the bounce levels' cost is not the camera rays'; DESIGN 9)
+            # 1.31 ms, the bounce levels' cost is not the camera rays'; DESIGN 6.2)
             try:
                 sharded = NativeShardedFrame(rend, device=torch.device("cuda", device), balanced=balanced_deal)
             except NativeCommUnavailable as e:   # raised on every rank together: same gather via torch's RCCL

@@ -187,7 +187,7 @@ def _cam(rt, W, H, pos, fwd, right, up):
 
 
 def grazing_cameras(rt, W, H):
-    """Cameras aimed at the wave walk's open case (VERDICT r5, DESIGN 4b): camera rays that graze a
+    """Cameras aimed at the wave walk's open case (VERDICT r5, DESIGN 2.3): camera rays that graze a
     triangle's plane, where the computed triangle t carries the most rounding error relative to its
     leaf box's entry.  TEAPOT-F: the eye at the floor's height (y = -1.225) looking along the floor,
     and just above it looking slightly down (every floor hit grazing); mig29 x16: the eye in the plane

@@ -847,7 +847,7 @@ def tile_pixels(W, H, tiles):
 @pytest.mark.parametrize("W,H,frames", [(1920, 1080, 5), (3840, 2160, 5)])
 def test_wave_walk_config4_full_size_bit_exact(rt, scenes, W, H, frames):
     """Config 4 (mig29 x16, primary + shadow) with RT_WALK_WAVE forced on every frame -- the walk
-    the timed choice picks for it (DESIGN 4b): RGB8, accumulator bits and the shadow-ray count of
+    the timed choice picks for it (DESIGN 4.2): RGB8, accumulator bits and the shadow-ray count of
     every frame against the oracle's IntersectBVH order (template/scene.h:285-320).  Then two
     frames with RT_WALK_CHECK_VERIFY: every walked lane is re-traced in the reference order and
     compared -- no lane may differ -- and the walk's counters (rays walked, lanes re-traced, boxes

@@ -1,6 +1,6 @@
 """Pin the CPU restatement (oracle/) against outputs of the reference itself.
 
-The reference is unbuildable in this image without stand-in headers (see DESIGN.md),
+The reference is unbuildable in this image without stand-in headers (see DESIGN.md 2.1),
 so the pins are the reference-run statistics recorded in SURVEY.md / BASELINE.md
 (plain-BVH build, single thread, the shipped global RNG seeded 0x12345678, the
 SURVEY Appendix A driver sequence).  Every integer below is copied from those runs.

@@ -1,6 +1,6 @@
 """The wave camera walk's exactness precondition, checked exhaustively with the oracle (CPU).
 
-DESIGN 4b: the walk (rt_kernels.inc wave_closest_hit_fast) returns IntersectBVH's answer R for a
+DESIGN 2.3: the walk (rt_kernels.inc wave_closest_hit_fast) returns IntersectBVH's answer R for a
 camera ray -- or flags the lane and re-traces it in the reference order -- unless R lies in a box the
 walk culled; and that needs R's computed t to lie more than the cull margin (2^-18) before its own
 leaf box's computed entry, with R in a box that is not sticky (sticky boxes -- those above a sphere,

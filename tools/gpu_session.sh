@@ -52,7 +52,7 @@ for s in "$@"; do
             step pab_c3 300 python tools/ab.py variants/prim_eager.so variants/prim_lazy.so --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
             step pab_c5 300 python tools/ab.py variants/prim_eager.so variants/prim_lazy.so --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
             unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
-        pairab)    # leaf loops taking two slots per round trip (frame kernels / also the lane kernel) against one  [historical: the variant was removed again after this A/B, DESIGN.md 10]
+        pairab)    # leaf loops taking two slots per round trip (frame kernels / also the lane kernel) against one  [historical: the variant was removed again after this A/B, docs/ROUND_LOG.md 10]
             export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
             V="variants/pair_all.so variants/pair_frame.so variants/pair_none.so"
             step prab_tp 300 python tools/ab.py $V --scene teapotF --rounds 9 --frames 60 --check
@@ -61,7 +61,7 @@ for s in "$@"; do
             step prab_c3 300 python tools/ab.py $V --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
             step prab_c5 300 python tools/ab.py $V --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
             unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
-        slabab)    # slab test as three packed pairs (v_pk_add_f32 / v_pk_mul_f32) against six scalar products  [historical: the variant was removed again after this A/B, DESIGN.md 10]
+        slabab)    # slab test as three packed pairs (v_pk_add_f32 / v_pk_mul_f32) against six scalar products  [historical: the variant was removed again after this A/B, docs/ROUND_LOG.md 10]
             export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
             V="variants/slab_pk.so variants/slab_sc.so"
             step slab_tp 300 python tools/ab.py $V --scene teapotF --rounds 9 --frames 60 --check
@@ -70,7 +70,7 @@ for s in "$@"; do
             step slab_c3 300 python tools/ab.py $V --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
             step slab_c5 300 python tools/ab.py $V --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
             unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
-        divab)     # triangle quotients skipped when the numerator decides the reject, against always dividing  [historical: the variant was removed again after this A/B, DESIGN.md 10]
+        divab)     # triangle quotients skipped when the numerator decides the reject, against always dividing  [historical: the variant was removed again after this A/B, docs/ROUND_LOG.md 10]
             export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
             V="variants/div1.so variants/div0.so"
             step div_tp 300 python tools/ab.py $V --scene teapotF --rounds 9 --frames 60 --check
@@ -79,7 +79,7 @@ for s in "$@"; do
             step div_c3 300 python tools/ab.py $V --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
             step div_c5 300 python tools/ab.py $V --scene cfg5 --spp 16 --depth 10 --rounds 7 --frames 6 --check
             unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
-        topab)     # the stack's top entry in a register (pop without an LDS read first) against the plain LDS stack  [historical: the variant was removed again after this A/B, DESIGN.md 10]
+        topab)     # the stack's top entry in a register (pop without an LDS read first) against the plain LDS stack  [historical: the variant was removed again after this A/B, docs/ROUND_LOG.md 10]
             export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
             V="variants/top1.so variants/top0.so"
             step top_tp 300 python tools/ab.py $V --scene teapotF --rounds 9 --frames 60 --check
@@ -102,7 +102,7 @@ for s in "$@"; do
             step ptk_c3 400 python tools/ab.py $V --scene cfg3 --spp 4 --depth 4 --rounds 7 --frames 10 --check
             step ptk_c5 400 python tools/ab.py $V --scene cfg5 --spp 16 --depth 10 --rounds 5 --frames 6 --check
             unset RT_PS_PIPELINE RT_PT_PIPELINE GPU_MAX_HW_QUEUES ;;
-        wsab)      # shadow rays on a wave-coherent any-hit walk (with the camera walk) against per-lane IsOccluded  [historical: the variant was removed again after this A/B, DESIGN.md 10]
+        wsab)      # shadow rays on a wave-coherent any-hit walk (with the camera walk) against per-lane IsOccluded  [historical: the variant was removed again after this A/B, docs/ROUND_LOG.md 10]
             export RT_PS_PIPELINE=0 RT_PT_PIPELINE=0 GPU_MAX_HW_QUEUES=8
             V="variants/ws1.so variants/ws0.so"
             step ws_mig 300 env RT_WAVE_PRIMARY=1 python tools/ab.py $V --scene mig16 --rounds 9 --frames 30 --check
@@ -180,7 +180,7 @@ for s in "$@"; do
             step d8q16f8 300 env GPU_MAX_HW_QUEUES=16 RT_PS_PIPELINE=1 RT_PS_DEPTH=8 $M8
             step d8q16f4 300 env GPU_MAX_HW_QUEUES=16 RT_PS_PIPELINE=1 RT_PS_DEPTH=4 $M8
             step d8q8f8 300 env GPU_MAX_HW_QUEUES=8 RT_PS_PIPELINE=1 RT_PS_DEPTH=8 $M8 ;;
-        prio)      # raised wave priority (s_setprio 3) for the leading fraction of the measured tile order  [historical: the variant was removed again after this A/B, DESIGN.md 10]
+        prio)      # raised wave priority (s_setprio 3) for the leading fraction of the measured tile order  [historical: the variant was removed again after this A/B, docs/ROUND_LOG.md 10]
             M8="python tools/shard_time.py --scene mig16 --strong --ns 1,8 --ranks last --deal balanced --out gpurun_out/prio.jsonl"
             for rep in 1 2; do
                 for pf in 0 0.03 0.1 0.3; do step prio_${pf}_$rep 300 env GPU_MAX_HW_QUEUES=8 RT_PRIO_FRAC=$pf $M8; done
@@ -200,7 +200,7 @@ for s in "$@"; do
             M8="python tools/shard_time.py --scene mig16 --strong --ns 8 --ranks last --deal balanced --frames 200"
             step m8_sq 300 env GPU_MAX_HW_QUEUES=8 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d gpurun_out/m8pmc/sq -o pmc --output-format csv -- $M8
             step m8_tcc 300 env GPU_MAX_HW_QUEUES=8 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/m8pmc/tcc -o pmc --output-format csv -- $M8 ;;
-        finprio)   # overlapped frames' finishing passes on a high-priority stream (RT_FIN_PRIO=1) against the caller's stream  [historical: the variant was removed again after this A/B, DESIGN.md 10]
+        finprio)   # overlapped frames' finishing passes on a high-priority stream (RT_FIN_PRIO=1) against the caller's stream  [historical: the variant was removed again after this A/B, docs/ROUND_LOG.md 10]
             for rep in 1 2; do
                 for fp in 0 1; do
                     step fp_m_${fp}_$rep 300 env GPU_MAX_HW_QUEUES=8 RT_FIN_PRIO=$fp python tools/shard_time.py --scene mig16 --strong --ns 1,4,8 --ranks last --deal balanced --out gpurun_out/finprio.jsonl

@@ -3,7 +3,7 @@
 
 The binding resource of the traversal kernels is vector issue, not HBM: the scenes are
 cache-resident (TEAPOT-F ~0.1 MB, mig29 x16 ~15 MB) and the per-launch HBM bytes the PMC
-counters see are the accumulator / frame traffic (DESIGN.md 4).  So `frac` is the VALU
+counters see are the accumulator / frame traffic (DESIGN.md 5).  So `frac` is the VALU
 issue fraction of the dominant kernel:
 
     frac = SQ_INSTS_VALU x 2 cycles / (1,024 SIMDs x launch cycles)

@@ -333,21 +333,22 @@ EXTRA_CONFIGS = {
 }
 
 
-def extra_config(cfg_no, world, rank, device, dist, stream, summary, warm_s=1.5, max_warm_s=12.0):
+def extra_config(cfg_no, world, rank, device, dist, stream, summary, backend="nccl", warm_s=1.5, max_warm_s=12.0):
     """One more BASELINE.json config (EXTRA_CONFIGS) beside the default headline, in the same process
     after it, so the driver's own runs time every GPU config: config 4 (mig29 x16, 1080p, 1 spp,
     primary + shadow) is north_star's strong-scaling case -- ONE frame split over the N ranks with the
     cost-balanced deal (RT_MULTI_BALANCED); config 3 (CFG3-sub, 4 spp, depth 4) is weak (each rank a
     1/N shard at spp 4N, interleaved deal); config 5 (CFG5-sub, 16 spp, depth 10) is strong (one
     frame split, interleaved deal: the bounce levels' cost is not the camera rays').  All go
-    through rt_render_frame_multi (pipelined) at N > 1 and through Tick at N = 1.
+    through rt_render_frame_multi (pipelined) at N > 1 and through Tick at N = 1 (with
+    RT_DIST_BACKEND=gloo, the rehearsal on one card, through ShardedFrame's torch.distributed gather).
     Warm-up: blocks of frames until warm_s seconds have passed (and, for config 4 at N > 1, every
     rank renders under the balanced deal; the renderer's timed choices re-run on the new deal's
     tiles), agreed over the ranks.  Then `frames` frames timed between a barrier + synchronize on
     both sides, max over ranks; then an untimed instrumented pass for every rank's render /
     exposed-gather split.  The roofline row is the config's dominant kernel from the tracked PMC
     summary (serial frames)."""
-    from advancedgraphicsraytracer_amd.distributed import NativeShardedFrame
+    from advancedgraphicsraytracer_amd.distributed import NativeCommUnavailable, NativeShardedFrame, ShardedFrame
     ec = EXTRA_CONFIGS[cfg_no]
     W, H, depth = 1920, 1080, ec["depth"]
     spp = ec["spp"] * world if ec["scaling"] == "weak" else ec["spp"]
@@ -357,7 +358,16 @@ def extra_config(cfg_no, world, rank, device, dist, stream, summary, warm_s=1.5,
     rx = rt.Renderer(sc, W, H)
     out = torch.zeros(W * H, dtype=torch.int32, device=dev)
     sptr = stream.cuda_stream
-    sf = NativeShardedFrame(rx, device=torch.device("cuda", device), balanced=ec["balanced"]) if world > 1 else None
+    sf, native = None, False
+    if world > 1:
+        if backend == "nccl":
+            try:
+                sf = NativeShardedFrame(rx, device=torch.device("cuda", device), balanced=ec["balanced"])
+                native = True
+            except NativeCommUnavailable:   # raised on every rank together: torch's gather instead
+                sf = None
+        if sf is None:
+            sf = ShardedFrame(rx, device=torch.device("cuda", device))
 
     def step(i):
         with torch.cuda.stream(stream):
@@ -380,7 +390,7 @@ def extra_config(cfg_no, world, rank, device, dist, stream, summary, warm_s=1.5,
         drain()
         torch.cuda.synchronize(device)
         el = time.perf_counter() - t0
-        ready = el >= warm_s and (sf is None or not ec["balanced"] or sf.deal_info()["balanced"] == 1)
+        ready = el >= warm_s and (not native or not ec["balanced"] or sf.deal_info()["balanced"] == 1)
         go = torch.tensor([1 if (ready or el > max_warm_s) else 0], device=dev)
         if dist:
             dist.all_reduce(go, op=dist.ReduceOp.MIN)
@@ -408,24 +418,27 @@ def extra_config(cfg_no, world, rank, device, dist, stream, summary, warm_s=1.5,
            "scene": ec["scene"], "spp": spp, "depth": depth, "scaling": ec["scaling"], "frames": frames,
            "warm_frames": nf}
     if sf is not None:
-        sf.set_timing(True)
-        for k in range(min(frames, 20)):
-            step(nf + frames + k)
-        drain()
-        torch.cuda.synchronize(device)
-        rms, gms, n = sf.timing()
-        mine = torch.tensor([rms / max(n, 1), gms / max(n, 1)], dtype=torch.float64, device=dev)
-        every = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(every, mine)
         dist.all_reduce(rays, op=dist.ReduceOp.SUM)
         dist.all_reduce(wall, op=dist.ReduceOp.MAX)
-        di = sf.deal_info()
-        res.update(path="rt_render_frame_multi (pipelined, %s)" % ("RT_MULTI_BALANCED" if ec["balanced"] else "interleaved deal"),
-                   deal_rank0={"in_use": "balanced" if di["balanced"] else "interleaved", **di},
-                   render_ms_per_frame_by_rank=[round(e[0].item(), 4) for e in every],
-                   # per rank max(0, gather end - render end); rank 0 receives without waiting for its own
-                   # render, so its figure is how much later than its own tiles the peers' arrived
-                   gather_ms_per_frame_by_rank=[round(e[1].item(), 4) for e in every])
+        if native:
+            sf.set_timing(True)
+            for k in range(min(frames, 20)):
+                step(nf + frames + k)
+            drain()
+            torch.cuda.synchronize(device)
+            rms, gms, n = sf.timing()
+            mine = torch.tensor([rms / max(n, 1), gms / max(n, 1)], dtype=torch.float64, device=dev)
+            every = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(every, mine)
+            di = sf.deal_info()
+            res.update(path="rt_render_frame_multi (pipelined, %s)" % ("RT_MULTI_BALANCED" if ec["balanced"] else "interleaved deal"),
+                       deal_rank0={"in_use": "balanced" if di["balanced"] else "interleaved", **di},
+                       render_ms_per_frame_by_rank=[round(e[0].item(), 4) for e in every],
+                       # per rank max(0, gather end - render end); rank 0 receives without waiting for its own
+                       # render, so its figure is how much later than its own tiles the peers' arrived
+                       gather_ms_per_frame_by_rank=[round(e[1].item(), 4) for e in every])
+        else:
+            res.update(path=f"ShardedFrame (torch.distributed gather, {backend}; interleaved deal)")
         sf.close()
     else:
         res.update(path="Renderer.Tick", in_flight=rx.overlap_depth()[0])
@@ -646,8 +659,7 @@ def main():
     extras = {}
     default_cfg2 = (args.config, args.scene, W, H, args.spp, args.depth) == (2, "teapotF", 1920, 1080, 1, 1)
     extra_list = [int(c) for c in args.extra_configs.split(",") if c.strip()] if not args.no_strong else []
-    if default_cfg2 and extra_list and (world == 1 or sharded is not None and native_fallback is None
-                                        and backend == "nccl"):
+    if default_cfg2 and extra_list:
         if sharded is not None:   # the headline communicator is done (its frames are flushed)
             sharded.close()
             sharded = None
@@ -656,11 +668,14 @@ def main():
         rend.close()
         summary_x = rl.load(args.summary)
         for c in extra_list:
-            ec = extra_config(c, world, rank, device, dist, stream, summary_x)
+            try:   # deterministic code and collectives that fail on every rank together: all ranks agree
+                ec = extra_config(c, world, rank, device, dist, stream, summary_x, backend=backend)
+            except Exception as e:   # the headline line still prints; the failure is reported in it
+                ec = {"error": f"{type(e).__name__}: {str(e)[:300]}"}
             extras[EXTRA_CONFIGS[c]["key"]] = ec
             if rank == 0:
-                print(f"bench: config {c}: {ec['ms_per_frame']} ms per frame, {ec['mrays_s']} Mrays/s",
-                      file=sys.stderr, flush=True)
+                print(f"bench: config {c}: " + (f"{ec['ms_per_frame']} ms per frame, {ec['mrays_s']} Mrays/s"
+                                                 if "error" not in ec else ec["error"]), file=sys.stderr, flush=True)
     companion = None
     if world == 1 and args.depth == 1 and (W, H) == (1920, 1080) and not args.no_companion:   # the metric's other frame size
         # the measured renderer is done: free its streams first, so that the companion's

@@ -442,12 +442,12 @@ inline f3 tvec_host(float4 r0, float4 r1, float4 r2, f3 a) {
 
 // The wave camera walk's sticky boxes (rt_kernels.inc, wave_closest_hit_fast): a node with a
 // primitive below it whose computed t can lie well before its leaf box's entry -- a sliver
-// triangle (its smallest corner angle under 2^RT_WALK_STICKY rad, default 2^-10: the common
+// triangle (its smallest corner angle's sine under 2^RT_WALK_STICKY, default 2^-8: the common
 // denominator of t, u, v is then mostly rounding, Primitive.h:255-273), a sphere (t = -b - sqrt(d)
 // near a tangent, Primitive.h:150-177) or a quad -- gets b.w = 1, and the walk culls it only on a
 // slab miss.  Computed in double on the float vertices; the lane traversals never read b.w.
 void mark_sticky(const Bvh &b, const rt_scene_desc *d, std::vector<float4> &nodes, std::vector<uint8_t> &sticky) {
-    double lim = std::ldexp(1.0, -10);
+    double lim = std::ldexp(1.0, -8);
     if (const char *e = std::getenv("RT_WALK_STICKY")) lim = std::atoi(e) >= 0 ? 0.0 : std::ldexp(1.0, std::atoi(e));
     bool spheres = true;   // RT_WALK_STICKY_SPHERES=0: A/B only
     if (const char *e = std::getenv("RT_WALK_STICKY_SPHERES")) spheres = std::atoi(e) != 0;
@@ -823,7 +823,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         }
     }
     // the wave walk's cull margin: RT_WALK_MARGIN = its base-2 exponent
-    v.walk_margin = 0x1p-18f;
+    v.walk_margin = 0x1p-12f;
     if (const char *e = std::getenv("RT_WALK_MARGIN")) v.walk_margin = std::ldexp(1.0f, std::max(-40, std::min(-1, std::atoi(e))));
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
     v.wave_primary = 0;

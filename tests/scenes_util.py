@@ -219,7 +219,7 @@ def grazing_cameras(rt, W, H):
     return out
 
 
-def sticky_prims(rt, prims, log2_lim=-10):
+def sticky_prims(rt, prims, log2_lim=-8):
     """The primitives whose boxes the wave camera walk never culls by distance (rt_device.hip
     mark_sticky): spheres, quads and sliver triangles (smallest corner angle's sine under
     2^log2_lim, from the float vertices in double)."""

@@ -445,8 +445,10 @@ inline f3 tvec_host(float4 r0, float4 r1, float4 r2, f3 a) {
 // triangle (its smallest corner angle's sine under 2^RT_WALK_STICKY, default 2^-8: the common
 // denominator of t, u, v is then mostly rounding, Primitive.h:255-273), a sphere (t = -b - sqrt(d)
 // near a tangent, Primitive.h:150-177) or a quad -- gets b.w = 1, and the walk culls it only on a
-// slab miss.  Computed in double on the float vertices; the lane traversals never read b.w.
-void mark_sticky(const Bvh &b, const rt_scene_desc *d, std::vector<float4> &nodes, std::vector<uint8_t> &sticky) {
+// slab miss.  Computed in double on the float vertices.  b.w then holds the walk's cull margin per
+// node: `margin` (SceneView::walk_margin), +inf for a sticky node; the lane traversals never read it.
+void mark_sticky(const Bvh &b, const rt_scene_desc *d, std::vector<float4> &nodes, std::vector<uint8_t> &sticky,
+                 float margin) {
     double lim = std::ldexp(1.0, -8);
     if (const char *e = std::getenv("RT_WALK_STICKY")) lim = std::atoi(e) >= 0 ? 0.0 : std::ldexp(1.0, std::atoi(e));
     bool spheres = true;   // RT_WALK_STICKY_SPHERES=0: A/B only
@@ -480,7 +482,10 @@ void mark_sticky(const Bvh &b, const rt_scene_desc *d, std::vector<float4> &node
         for (uint32_t j = i; st && j != ~0u && nodes[2 * j + 1].w == 0.0f; j = parent[j]) nodes[2 * j + 1].w = 1.0f;
     }
     sticky.assign(used, 0);
-    for (uint32_t i = 0; i < used; ++i) sticky[i] = nodes[2 * i + 1].w != 0.0f;
+    for (uint32_t i = 0; i < used; ++i) {
+        sticky[i] = nodes[2 * i + 1].w != 0.0f;
+        nodes[2 * i + 1].w = sticky[i] ? HUGE_VALF : margin;
+    }
 }
 
 int scene_create(const rt_scene_desc *d, rt_scene **out) {
@@ -570,7 +575,7 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
     if (s->bvh.depth > 64) { delete s; return fail(RT_ERR_UNSUPPORTED, "BVH deeper than 64 (the reference's stack[64])"); }
     s->stack_depth = pick_stack(s->bvh.depth);
     // trees deeper than 60: the lane stacks (depth x 1 KB) leave no room for the walk's words
-    s->walk_fits = (size_t)s->stack_depth * (256u + 4u * 2u) * sizeof(uint32_t) <= kLdsLaunchMax;
+    s->walk_fits = (size_t)s->stack_depth * (256u + 4u) * sizeof(uint32_t) <= kLdsLaunchMax;
 
     // ---- device node array: packed (leftFirst << 8 | count) word in b.z
     std::vector<float4> nodes(2 * (size_t)s->bvh.nodes_used);
@@ -581,7 +586,11 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
         nodes[2 * i + 1] = make_float4(nd.mx[1], nd.mx[2], ubits(word), 0.0f);
     }
     std::vector<uint8_t> sticky;
-    mark_sticky(s->bvh, d, nodes, sticky);
+    // the wave walk's cull margin (DESIGN 2.3): RT_WALK_MARGIN = its base-2 exponent
+    s->view.walk_margin = 0x1p-12f;
+    if (const char *e = std::getenv("RT_WALK_MARGIN"))
+        s->view.walk_margin = std::ldexp(1.0f, std::max(-40, std::min(-1, std::atoi(e))));
+    mark_sticky(s->bvh, d, nodes, sticky, s->view.walk_margin);
     std::vector<float4> quads;
     uint32_t quad_root = 0;
     {
@@ -822,9 +831,6 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
                 if (!(ch.mn[a] >= nd.mn[a]) || !(ch.mx[a] <= nd.mx[a])) s->nested = false;
         }
     }
-    // the wave walk's cull margin (DESIGN 2.3): RT_WALK_MARGIN = its base-2 exponent
-    v.walk_margin = 0x1p-12f;
-    if (const char *e = std::getenv("RT_WALK_MARGIN")) v.walk_margin = std::ldexp(1.0f, std::max(-40, std::min(-1, std::atoi(e))));
     // camera-ray walk: wave-coherent vs per-lane (RT_WAVE_PRIMARY=0/1 overrides the policy)
     v.wave_primary = 0;
     const bool wave_ok = !s->has_cubes && s->nested && s->walk_fits;
@@ -843,9 +849,9 @@ int scene_create(const rt_scene_desc *d, rt_scene **out) {
 
 size_t stack_bytes(const rt_scene *s) { return (size_t)s->stack_depth * 256u * sizeof(uint32_t); }
 // launches whose camera rays may take the wave walk (SceneView::wave_primary) also hold each wave's
-// uniform stack of (node word, sticky) pairs past the lane stacks (walk_words in rt_kernels.inc): 4 waves x depth
+// uniform stack of node words past the lane stacks (walk_words in rt_kernels.inc): 4 waves x depth
 size_t walk_bytes(const rt_scene *s, const SceneView &v) {
-    return v.wave_primary ? (size_t)s->stack_depth * 4u * 2u * sizeof(uint32_t) : 0u;
+    return v.wave_primary ? (size_t)s->stack_depth * 4u * sizeof(uint32_t) : 0u;
 }
 // the compiled MAXD class a Trace depth runs in
 int max_depth_class(uint32_t depth) { return depth <= 1 ? 1 : depth <= 4 ? 4 : depth <= 10 ? 10 : 32; }

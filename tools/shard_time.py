@@ -40,15 +40,17 @@ def time_share(scene, a, spp, frames, render):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     with torch.cuda.stream(st):
         ev[0].record()
+        h0 = time.perf_counter()
         for f in range(frames):
             render(r, spp, 100000 + f, st.cuda_stream)
+        h1 = time.perf_counter()
         ev[1].record()
     torch.cuda.synchronize()
     c1 = r.counters()
     ms = ev[0].elapsed_time(ev[1]) / frames
     rays = sum(c1[k] - c0[k] for k in ("primary", "shadow", "bounce")) / frames
     od = r.overlap_depth()
-    out = {"ms": round(ms, 4), "mrays": round(rays / 1e6, 3), "in_flight": od[0], "choices": r.choices(),
+    out = {"ms": round(ms, 4), "host_ms": round((h1 - h0) * 1e3 / frames, 4), "mrays": round(rays / 1e6, 3), "in_flight": od[0], "choices": r.choices(),
            "in_flight_groups_ms": [round(float(x), 4) for x in od[1]]}
     cost = r.tile_costs().astype(np.float64)
     if cost.size:

@@ -60,6 +60,43 @@ def time_share(scene, a, spp, frames, render):
     return out, cost
 
 
+def spread_deal(w, h, n, cost, nheavy):
+    """tile lists per rank: the nheavy costliest tiles snake-dealt, the rest cut in Morton order so
+    that every rank's summed cost is the frame's / n (as far as whole tiles allow)"""
+    tx, ty = (w + 7) // 8, (h + 7) // 8
+    nt = tx * ty
+    cost = np.asarray(cost, dtype=np.float64)
+    order = np.argsort(-cost, kind="stable")
+    heavy = order[:nheavy]
+    owner = -np.ones(nt, dtype=np.int64)
+    hsum = np.zeros(n)
+    for i, t in enumerate(heavy):
+        k = i % n if (i // n) % 2 == 0 else n - 1 - i % n
+        owner[t] = k
+        hsum[k] += cost[t]
+
+    def morton(x, y):
+        m = 0
+        for b in range(16):
+            m |= ((x >> b) & 1) << (2 * b) | ((y >> b) & 1) << (2 * b + 1)
+        return m
+    rest = [t for t in range(nt) if owner[t] < 0]
+    rest.sort(key=lambda t: morton(t % tx, t // tx))
+    rc = cost[rest]
+    pre = np.concatenate([[0.0], np.cumsum(rc)])
+    target = cost.sum() / n
+    cum, start = 0.0, 0
+    for k in range(n):
+        cum += max(0.0, target - hsum[k])
+        end = len(rest) if k == n - 1 else int(np.clip(np.searchsorted(pre, cum), start, len(rest)))
+        for t in rest[start:end]:
+            owner[t] = k
+        start = end
+    tiles = np.concatenate([np.nonzero(owner == k)[0] for k in range(n)]).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum([(owner == k).sum() for k in range(n)])]).astype(np.int64)
+    return tiles, off
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scene", default="teapotF")
@@ -93,7 +130,7 @@ def main():
     full_cost = None
     deals = a.deal.split(",")
     work_map = None
-    if "balanced" in deals:   # the product's deal input: deterministic, no timing needed
+    if "balanced" in deals or any(d.startswith("spread") for d in deals):   # the product's deal input
         rw = rt.Renderer(scene, a.w, a.h)
         work_map = rw.tile_work(spp=a.spp if a.strong else a.spp * ns[0], depth=a.depth, frame=100000)
         rw.close()
@@ -117,6 +154,10 @@ def main():
                 tiles, off = rt.tile_deal(a.w, a.h, n, work_map)
             elif deal == "balanced_cycles":
                 tiles, off = rt.tile_deal(a.w, a.h, n, full_cost if (full_cost is not None and full_cost.size) else None)
+            elif deal.startswith("spread"):   # spreadK: the K*n costliest tiles (work map) dealt snake-wise, the
+                # rest in Morton runs that even out each rank's total work (heavy chains shared out)
+                K = int(deal[6:] or 4)
+                tiles, off = spread_deal(a.w, a.h, n, work_map, K * n)
             elif deal.startswith("blocks"):   # blocksB: BxB-tile blocks dealt round-robin (block b -> rank b % n)
                 B = int(deal[6:] or 8)
                 tx, ty = (a.w + 7) // 8, (a.h + 7) // 8
@@ -130,7 +171,7 @@ def main():
             ranks = range(n) if a.ranks == "all" else [n - 1]
             per = []
             for k in ranks:
-                if deal.startswith("balanced") or deal.startswith("blocks"):
+                if deal.startswith("balanced") or deal.startswith("blocks") or deal.startswith("spread"):
                     mine = tiles[off[k]:off[k + 1]]
                     render = lambda r, spp_, fr, s, mine=mine: r.render_shard_tiles(buf, mine, spp=spp_, depth=a.depth, frame=fr, stream=s)
                 else:

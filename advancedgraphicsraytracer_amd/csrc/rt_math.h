@@ -82,5 +82,9 @@ RT_HD uint32_t init_seed(uint32_t base) {
 }
 RT_HD uint32_t rnd_u(uint32_t &s) { s ^= s << 13; s ^= s >> 17; s ^= s << 5; return s; }
 RT_HD float rnd_f(uint32_t &s) { return (float)rnd_u(s) * 2.3283064365387e-10f; }
+// rnd_f(s) * 2.0f - 1.0f with one rounding fewer to issue: the literal above is exactly 2^-32, so
+// both products are exact power-of-two scalings and the fma's single rounding is the subtraction's
+static_assert(2.3283064365387e-10f == 0x1p-32f, "rnd_f scales by exactly 2^-32");
+RT_HD float rnd_sym(uint32_t &s) { return __builtin_fmaf((float)rnd_u(s), 0x1p-31f, -1.0f); }
 
 }  // namespace rt
